@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched CRC32C over 4 KiB blocks on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg5]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A "step" = one pass of the hot path (nvl_crc32c_fixed_dev through the C ABI)
+over one batch of synthetic, already-HBM-resident 4 KiB blocks.
+
+Workloads (BASELINE.json configs):
+  cfg2 (default): 10^5 x 4 KiB blocks PER GPU (weak scaling).  Rank r holds
+        global blocks r, r+N, r+2N, ... (round-robin shard, generated in place
+        from the canonical splitmix64 stream).  At N=1 this is
+        exactly BASELINE config 2.
+  cfg5: 10^7 x 4 KiB blocks in total, round-robin over the N GPUs (strong).
+
+No data-path collective: every block's CRC is independent, so shards never
+exchange bytes; only the timing max and a verification digest cross ranks
+(outside the timed region).
+
+The JSON line adds
+  roofline     -- dominant kernel: algorithmic bytes per launch (4096+4 B per
+                  block) / its mean duration from HIP events recorded on the
+                  launch stream, against the 8 TB/s HBM3E peak.  `traffic` is
+                  the PMC-measured HBM bytes per launch from
+                  profiles/pmc_traffic.json when present (rocprofv3, corrected
+                  per MI355X_MICROARCH.md §HBM), else null.
+  cpu_baseline -- the reference's own util/crc32c.cc + port/port_posix_sse.cc
+                  (oracle/_ref, kind "reference"; the clean-room port, kind
+                  "port", if _ref is absent) timed on this host's cores on a
+                  bounded sample of the same blocks (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident batched CRC32C over 4 KiB blocks; % HBM-read roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BLOCK = 4096
+SEED_CFG2 = 0x5EED0001
+SEED_CFG5 = 0x5EED0005
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=["cfg2", "cfg5"], default="cfg2")
+    ap.add_argument("--blocks", type=int, default=None, help="override blocks per GPU (cfg2)")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0,
+                    help="target seconds per CPU-baseline leg (all-core and 1-thread)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time host->device->host end to end")
+    ap.add_argument("--verify", action="store_true", default=True)
+    return ap.parse_args()
+
+
+def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int) -> dict:
+    import oracle
+    kind = "reference" if oracle.ref_available("sse") else "port"
+    impl = oracle.ref("sse") if kind == "reference" else oracle.port()
+
+    def run(nblk, th):
+        if kind == "reference":
+            return impl.fixed_mt(host, BLOCK, BLOCK, nblk, th)
+        return impl.fixed_mt(host, BLOCK, BLOCK, nblk, th, False)
+
+    def timed(nblk, th):
+        run(min(nblk, 2000), th)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            r = run(nblk, th)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return r, reps * nblk * BLOCK / el / 2**30, reps, el
+
+    th = max(1, min(threads, os.cpu_count() or 1))
+    r_all, gibs_all, reps_all, el_all = timed(n, th)
+    r_one, gibs_one, reps_one, el_one = timed(min(n, 20000), 1)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(gibs_all, 3), "unit": "GiB/s", "cores": th, "kind": kind,
+        "sample": f"{reps_all} passes over the first {n} x 4 KiB blocks of this rank's batch "
+                  f"({el_all:.1f} s, {th} threads, contiguous partition), "
+                  f"leveldb::crc32c::Value via port::AcceleratedCRC32C (SSE4.2)",
+        "single_thread": {"value": round(gibs_one, 3), "unit": "GiB/s", "cores": 1,
+                          "sample": f"{reps_one} passes over {min(n, 20000)} blocks ({el_one:.1f} s)"},
+        "host_cpu": model, "host_nproc": os.cpu_count(),
+        "_check": r_all,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from nvlevelz_amd import crc32c
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"[bench] --gpus {args.gpus} needs torch.distributed.run; running 1 rank", file=sys.stderr)
+        args.gpus = world
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)  # RCCL; timing/verification only
+    crc32c.init(local)
+
+    N = world
+    if args.config == "cfg2":
+        n_local = args.blocks or 100_000
+        seed = SEED_CFG2
+        workload = (f"cfg2: {n_local} x 4 KiB blocks per GPU (BASELINE config 2 at N=1), device-resident, "
+                    f"stride 4096, round-robin global block ids rank+k*N")
+        scaling = "weak"
+    else:
+        total = 10_000_000
+        n_local = (total - rank + N - 1) // N
+        seed = SEED_CFG5
+        workload = f"cfg5: 10^7 x 4 KiB blocks total, round-robin over {N} GPU(s)"
+        scaling = "strong"
+
+    buf = torch.empty(n_local * BLOCK, dtype=torch.uint8, device=dev)
+    crc32c.fill_splitmix(buf, n_local, BLOCK, seed, first_block=rank, block_step=N)
+    out = torch.empty(n_local, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        crc32c.extend_fixed(buf, BLOCK, BLOCK, n_local, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # --- verification (untimed) --------------------------------------------
+    verify = {}
+    res = crc32c.to_u32(out)
+    if rank == 0:
+        if args.config == "cfg2":
+            verify["crc0"] = hex(int(res[0]))
+            verify["crc0_ok"] = int(res[0]) == 0x6104AC89
+            if N == 1 and n_local == 100_000:
+                import oracle
+                with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+                    g = json.load(f)["cfg2"]
+                d = oracle.port().digest(res)
+                verify["digest"] = hex(d)
+                verify["digest_ok"] = d == g["digest"]
+
+    # --- timed region ------------------------------------------------------
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        step()
+        ends[k].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nt = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(nt, op=dist.ReduceOp.SUM)
+        total_blocks = int(nt.item())
+    else:
+        total_blocks = n_local
+
+    value = total_blocks * BLOCK * args.steps / elapsed / 2**30
+    mean_kern_s = float(np.mean(kern_ms)) / 1e3
+    med_kern_s = float(np.median(kern_ms)) / 1e3
+    alg_bytes = n_local * (BLOCK + 4)  # every input byte once + 4 B CRC out
+    achieved = alg_bytes / mean_kern_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pj = json.load(f)
+            if pj.get("blocks") == n_local:
+                traffic = pj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    e2e = None
+    if rank == 0 and N == 1 and not args.no_cpu:
+        host = buf.cpu().numpy()
+        cpu = cpu_baseline(host, n_local, args.cpu_seconds, args.cpu_threads)
+        chk = cpu.pop("_check")
+        verify["cpu_matches_gpu"] = bool(np.array_equal(chk, res[:chk.size]))
+    if rank == 0 and args.e2e:
+        pinned = torch.empty(n_local * BLOCK, dtype=torch.uint8).pin_memory()
+        pinned.copy_(buf.cpu())
+        hp = pinned.numpy()
+        crc32c.extend_fixed_host(hp, BLOCK, BLOCK, n_local)
+        t1 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            r = crc32c.extend_fixed_host(hp, BLOCK, BLOCK, n_local)
+        el = time.perf_counter() - t1
+        e2e = {"value": round(n_local * BLOCK * reps / el / 2**30, 3), "unit": "GiB/s",
+               "what": "pinned host -> H2D -> kernel -> D2H of u32 results, 2-stream pipelined, synchronous",
+               "ok": bool(np.array_equal(r, res))}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": N,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 stream, SURVEY.md §8d), generated in HBM",
+            "config": {"workload": workload, "blocks_per_gpu": n_local, "block_bytes": BLOCK,
+                       "parallelism": f"{N} independent shard(s), no data-path collective"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "crc32c_fixed_kernel<true> (fast path)",
+                         "alg_bytes_per_launch": alg_bytes,
+                         "mean_launch_us": round(mean_kern_s * 1e6, 2),
+                         "median_launch_us": round(med_kern_s * 1e6, 2)},
+            "cpu_baseline": cpu,
+            "verify": verify,
+        }
+        if e2e:
+            line["e2e"] = e2e
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * include/nvl_crc32c.h -- C ABI of the MI355X-native CRC32C block-checksum
+ * engine (libnvl_crc32c.so).
+ *
+ * Drop-in boundary: this ABI sits beneath the reference's util/crc32c.h
+ * (/root/reference/util/crc32c.h:17-40) and replaces its backend seam
+ * port::AcceleratedCRC32C (/root/reference/port/port_posix.h:169, contract
+ * port/port_example.h:132-136, implementation port/port_posix_sse.cc:69-126).
+ * Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Semantics are bit-exact with leveldb::crc32c::Extend (util/crc32c.cc:299-347):
+ * CRC32C, reflected polynomial 0x82F63B78, register pre/post inverted, with
+ * Extend(crc, "", 0) == crc.
+ *
+ * Threading: every entry point is reentrant and thread-safe.  Device
+ * entry points are asynchronous on the HIP stream passed in `stream`
+ * (a hipStream_t; NULL = the null stream); inputs must stay valid and
+ * unmodified and outputs must not be read until that stream is synchronised.
+ * The library owns only its lookup tables (one small copy per device,
+ * created on first use or by nvl_crc32c_init) and, when the caller passes no
+ * workspace, stream-ordered scratch allocated and freed on `stream`.
+ *
+ * Errors: the reference has no error channel (its accelerator signals
+ * "unavailable" by returning 0, util/crc32c.cc:290-303).  Here every batch
+ * entry point returns an int status (NVL_CRC32C_OK = 0, negative on error)
+ * and writes nothing on argument errors.  There is NO silent CPU fallback in
+ * the batch entry points: a caller that wants one calls nvl_crc32c_extend
+ * itself on a non-zero status.
+ */
+#ifndef NVL_CRC32C_H_
+#define NVL_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NVL_CRC32C_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define NVL_API __attribute__((visibility("default")))
+#else
+#define NVL_API
+#endif
+
+/* status codes */
+#define NVL_CRC32C_OK 0
+#define NVL_CRC32C_EINVAL (-1)     /* bad argument (NULL pointer, size overflow) */
+#define NVL_CRC32C_EHIP (-2)       /* a HIP runtime call failed */
+#define NVL_CRC32C_ENODEV (-3)     /* no HIP device / device index out of range */
+#define NVL_CRC32C_ESELFTEST (-4)  /* GPU backend failed its known-answer probe */
+#define NVL_CRC32C_ENOSPC (-5)     /* caller workspace smaller than required */
+
+/* flags */
+#define NVL_CRC32C_FLAG_MASK 0x1u  /* store crc32c::Mask(crc) (util/crc32c.h:31-34),
+                                      i.e. the on-disk trailer/header value of
+                                      table/table_builder.cc:187 and
+                                      db/log_writer.cc:96 */
+
+/* ---- lifecycle ---------------------------------------------------------- */
+
+/* Build the lookup tables on `device` and run the known-answer probe
+ * "TestCRCBuffer" -> 0xdcbc59fa on the GPU (mirrors CanAccelerateCRC32C,
+ * util/crc32c.cc:290-297).  Optional: batch calls initialise lazily. */
+NVL_API int nvl_crc32c_init(int device);
+
+/* Release every device's tables.  No batch call may be in flight. */
+NVL_API int nvl_crc32c_shutdown(void);
+
+/* 1 if the GPU backend on the current device passed its probe, else 0. */
+NVL_API int nvl_crc32c_gpu_accelerated(void);
+
+/* Human-readable text for a status code. */
+NVL_API const char* nvl_crc32c_strerror(int status);
+
+/* ABI version (NVL_CRC32C_ABI_VERSION). */
+NVL_API int nvl_crc32c_abi_version(void);
+
+/* ---- single buffer, host memory (util/crc32c.h:17-40) -------------------- */
+/* These replace the reference's host path one-for-one.  One buffer of a few
+ * KiB is not worth a GPU round trip, so they run on the calling CPU thread
+ * (SSE4.2 crc32 instruction when present, else slice-by-8).  They are the
+ * reference API's per-call semantics, not a fallback of the batch calls. */
+
+/* util/crc32c.h:17 leveldb::crc32c::Extend */
+NVL_API uint32_t nvl_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
+/* util/crc32c.h:20-22 leveldb::crc32c::Value */
+NVL_API uint32_t nvl_crc32c_value(const void* data, size_t n);
+/* util/crc32c.h:31-34 leveldb::crc32c::Mask */
+NVL_API uint32_t nvl_crc32c_mask(uint32_t crc);
+/* util/crc32c.h:37-40 leveldb::crc32c::Unmask */
+NVL_API uint32_t nvl_crc32c_unmask(uint32_t masked_crc);
+
+/* ---- batched, device-resident (the hot path) ----------------------------- */
+
+/* Fixed-stride batch: buffer i is the `len` bytes at base + i*stride (device
+ * memory).  out[i] = Extend(init_i, buffer i, len) where init_i = init[i] if
+ * `init` (device array of n u32) is non-NULL, else `init_all`.  With
+ * NVL_CRC32C_FLAG_MASK, out[i] = Mask(that).  Replaces n calls of
+ * crc32c::Value/Extend at table/table_builder.cc:185-186 (data blocks of one
+ * table laid out back to back) and the db_bench crc32c loop
+ * (db/db_bench.cc:729-746).  Fast path when base and stride are multiples
+ * of 16 and len a multiple of 4096. */
+NVL_API int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len, uint64_t n,
+                         const uint32_t* init, uint32_t init_all, uint32_t* out,
+                         uint32_t flags, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* Workspace bytes nvl_crc32c_fixed_dev needs for this shape (0 when none). */
+NVL_API size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, uint64_t n);
+
+/* Variable-length batch: buffer i is lengths[i] bytes at base + offsets[i]
+ * (all three in device memory; pass base = NULL to give absolute device
+ * addresses in `offsets`).  Arbitrary alignment and length (0 included).
+ * out[i] = Extend(init_i, buffer i) (Mask()ed with NVL_CRC32C_FLAG_MASK).
+ * Replaces per-call Value/Extend at table/format.cc:90-92 (block verify),
+ * db/log_reader.cc:255-256 and db/log_writer.cc:95 (records). */
+NVL_API int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64_t* lengths,
+                         const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
+                         uint32_t flags, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* Workspace bytes nvl_crc32c_batch_dev needs for n buffers. */
+NVL_API size_t nvl_crc32c_batch_workspace_bytes(uint64_t n);
+
+/* ---- batched, host-resident (end-to-end path) ---------------------------- */
+
+/* Host buffers in, host results out, synchronous: stages the buffers through
+ * pinned memory, H2D, GPU batch kernel, D2H.  ptrs/lengths/init/out are host
+ * arrays (init may be NULL -> init_all).  This is what the block-batching
+ * shims at the four reference call sites use. */
+NVL_API int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths,
+                          const uint32_t* init, uint32_t init_all, uint32_t* out,
+                          uint64_t n, uint32_t flags);
+
+/* Host fixed-stride batch (one contiguous host region, e.g. an mmap'd table
+ * file or a pinned bench buffer), pipelined H2D/compute/D2H over two
+ * streams.  Synchronous. */
+NVL_API int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint64_t n,
+                          const uint32_t* init, uint32_t init_all, uint32_t* out,
+                          uint32_t flags);
+
+/* ---- synthetic inputs (measurement harness) -------------- */
+
+/* Fill device memory with the canonical splitmix64 byte stream: block k
+ * (block_bytes long, written at dst + k*block_bytes) receives stream bytes
+ * [(first_block + k*block_step)*block_bytes, +block_bytes), where stream word
+ * j is splitmix64's (j+1)-th output from state `seed`, little-endian.
+ * block_step > 1 lays out a round-robin shard (buffer i on GPU i mod G).
+ * block_bytes must be a multiple of 8.  Asynchronous on `stream`. */
+NVL_API int nvl_crc32c_fill_splitmix(void* dst, uint64_t nblocks, uint64_t block_bytes,
+                                     uint64_t first_block, uint64_t block_step, uint64_t seed,
+                                     void* stream);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* NVL_CRC32C_H_ */

@@ -1,0 +1,238 @@
+"""nvlevelz_amd.crc32c -- Python mirror of the reference's util/crc32c.h API
+plus the batched device-resident engine behind it.
+
+Reference interface (/root/reference/util/crc32c.h):
+    Extend(init_crc, data, n)  -> :func:`extend`       (crc32c.h:17)
+    Value(data, n)             -> :func:`value`        (crc32c.h:20-22)
+    kMaskDelta                 -> :data:`kMaskDelta`   (crc32c.h:24)
+    Mask(crc) / Unmask(m)      -> :func:`mask` / :func:`unmask` (crc32c.h:31-40)
+
+Batched, MI355X-resident (the hot path; HIP kernels via the C ABI):
+    :func:`extend_fixed`  -- n buffers at a fixed stride (SSTable data blocks,
+                             db_bench's 4 KiB crc32c loop)
+    :func:`extend_batch`  -- n buffers at arbitrary offsets/lengths
+    :func:`extend_batch_host`, :func:`extend_fixed_host` -- host memory in/out
+                             (pinned staging + H2D + kernel + D2H)
+
+The batch functions never fall back to the CPU: without a GPU, or if the
+GPU backend fails its known-answer probe (util/crc32c.cc:290-297 analogue),
+they raise :class:`Crc32cError`.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+from ._lib import Crc32cError, FLAG_MASK, check, lib
+
+kMaskDelta = 0xA282EAD8
+
+BytesLike = Union[bytes, bytearray, memoryview, np.ndarray]
+
+
+def _buf(data: BytesLike):
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data).view(np.uint8)
+        return a, a.ctypes.data, a.nbytes
+    b = bytes(data)
+    return b, b, len(b)
+
+
+# ---- util/crc32c.h API (host, one buffer) ---------------------------------
+
+def extend(init_crc: int, data: BytesLike) -> int:
+    """crc32c of concat(A, data) given init_crc = crc32c(A) (util/crc32c.h:14-17)."""
+    keep, ptr, n = _buf(data)
+    return lib.nvl_crc32c_extend(init_crc & 0xFFFFFFFF, ptr, n)
+
+
+def value(data: BytesLike) -> int:
+    """crc32c of data (util/crc32c.h:20-22)."""
+    keep, ptr, n = _buf(data)
+    return lib.nvl_crc32c_value(ptr, n)
+
+
+def mask(crc: int) -> int:
+    """Masked representation of crc: rotate right 15, add kMaskDelta (util/crc32c.h:31-34)."""
+    return lib.nvl_crc32c_mask(crc & 0xFFFFFFFF)
+
+
+def unmask(masked_crc: int) -> int:
+    """Inverse of :func:`mask` (util/crc32c.h:37-40)."""
+    return lib.nvl_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+
+
+# ---- device-resident batches ----------------------------------------------
+
+def _torch():
+    import torch  # plumbing only: device memory + streams
+    return torch
+
+
+def init(device: int = 0) -> None:
+    """Build tables on `device` and run the GPU known-answer probe."""
+    check(lib.nvl_crc32c_init(device), "nvl_crc32c_init")
+
+
+def gpu_accelerated() -> bool:
+    return bool(lib.nvl_crc32c_gpu_accelerated())
+
+
+def _stream_handle(t) -> int:
+    torch = _torch()
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _require_dev(t, name: str, dtype=None):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA(HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype not in dtype:
+        raise TypeError(f"{name} has dtype {t.dtype}, expected one of {dtype}")
+
+
+def fixed_workspace_bytes(stride: int, length: int, n: int) -> int:
+    return lib.nvl_crc32c_fixed_workspace_bytes(stride, length, n)
+
+
+def batch_workspace_bytes(n: int) -> int:
+    return lib.nvl_crc32c_batch_workspace_bytes(n)
+
+
+def extend_fixed(buf, stride: int, length: int, n: int, init=0, *, mask: bool = False,
+                 base_offset: int = 0, out=None, workspace=None):
+    """out[i] = Extend(init_i, buf[base_offset + i*stride : ... + length]).
+
+    ``buf`` is a uint8 device tensor; ``init`` an int (all buffers) or an
+    int32/uint32 device tensor of n values.  Returns an int32 device tensor
+    holding the u32 results (bit pattern).  Asynchronous on the current stream.
+    """
+    torch = _torch()
+    _require_dev(buf, "buf", (torch.uint8, torch.int8))
+    if n < 0 or length < 0 or stride < 0 or base_offset < 0:
+        raise ValueError("negative size")
+    if n and base_offset + (n - 1) * stride + length > buf.numel():
+        raise ValueError("batch extends past the end of buf")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=buf.device)
+    _require_dev(out, "out", (torch.int32, torch.uint32))
+    if out.numel() < n:
+        raise ValueError("out too small")
+    init_ptr, init_all = None, 0
+    if isinstance(init, int):
+        init_all = init & 0xFFFFFFFF
+    else:
+        _require_dev(init, "init", (torch.int32, torch.uint32))
+        if init.numel() < n:
+            raise ValueError("init too small")
+        init_ptr = init.data_ptr()
+    ws_ptr, ws_bytes = None, 0
+    if workspace is not None:
+        ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    rc = lib.nvl_crc32c_fixed_dev(buf.data_ptr() + base_offset, stride, length, n, init_ptr, init_all,
+                                  out.data_ptr(), FLAG_MASK if mask else 0, ws_ptr, ws_bytes,
+                                  _stream_handle(buf))
+    check(rc, "nvl_crc32c_fixed_dev")
+    return out
+
+
+def extend_batch(buf, offsets, lengths, init=0, *, mask: bool = False, out=None, workspace=None):
+    """out[i] = Extend(init_i, buf[offsets[i] : offsets[i] + lengths[i]]).
+
+    ``offsets``/``lengths`` are int64 device tensors (u64 bit patterns).
+    Arbitrary alignment and lengths (0 included).  Asynchronous.
+    """
+    torch = _torch()
+    _require_dev(buf, "buf", (torch.uint8, torch.int8))
+    _require_dev(offsets, "offsets", (torch.int64, torch.uint64))
+    _require_dev(lengths, "lengths", (torch.int64, torch.uint64))
+    n = offsets.numel()
+    if lengths.numel() != n:
+        raise ValueError("offsets and lengths differ in size")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=buf.device)
+    _require_dev(out, "out", (torch.int32, torch.uint32))
+    init_ptr, init_all = None, 0
+    if isinstance(init, int):
+        init_all = init & 0xFFFFFFFF
+    else:
+        _require_dev(init, "init", (torch.int32, torch.uint32))
+        init_ptr = init.data_ptr()
+    ws_ptr, ws_bytes = None, 0
+    if workspace is not None:
+        ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    rc = lib.nvl_crc32c_batch_dev(buf.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), init_ptr, init_all,
+                                  out.data_ptr(), n, FLAG_MASK if mask else 0, ws_ptr, ws_bytes,
+                                  _stream_handle(buf))
+    check(rc, "nvl_crc32c_batch_dev")
+    return out
+
+
+def extend_batch_host(buffers: Sequence[BytesLike], init: Union[int, Sequence[int]] = 0, *,
+                      mask: bool = False) -> np.ndarray:
+    """Host buffers in, u32 CRCs out (synchronous; pinned staging + GPU)."""
+    import ctypes
+    n = len(buffers)
+    keep = [_buf(b) for b in buffers]
+    ptrs = (ctypes.c_void_p * max(n, 1))()
+    lens = np.empty(n, dtype=np.uint64)
+    for i, (obj, p, m) in enumerate(keep):
+        ptrs[i] = ctypes.cast(ctypes.c_char_p(obj), ctypes.c_void_p).value if isinstance(obj, bytes) else p
+        lens[i] = m
+    out = np.empty(n, dtype=np.uint32)
+    init_ptr, init_all = None, 0
+    if isinstance(init, int):
+        init_all = init & 0xFFFFFFFF
+    else:
+        ini = np.ascontiguousarray(np.asarray(init, dtype=np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
+        init_ptr = ini.ctypes.data
+    rc = lib.nvl_crc32c_batch_host(ptrs, lens.ctypes.data, init_ptr, init_all, out.ctypes.data, n,
+                                   FLAG_MASK if mask else 0)
+    check(rc, "nvl_crc32c_batch_host")
+    return out
+
+
+def extend_fixed_host(buf: np.ndarray, stride: int, length: int, n: int, init=0, *,
+                      mask: bool = False) -> np.ndarray:
+    """Fixed-stride batch over one contiguous host region (pinned is fastest)."""
+    a = buf if isinstance(buf, np.ndarray) else np.frombuffer(buf, dtype=np.uint8)
+    if n and (n - 1) * stride + length > a.nbytes:
+        raise ValueError("batch extends past the end of buf")
+    out = np.empty(n, dtype=np.uint32)
+    init_ptr, init_all = None, 0
+    if isinstance(init, int):
+        init_all = init & 0xFFFFFFFF
+    else:
+        ini = np.ascontiguousarray(np.asarray(init, dtype=np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
+        init_ptr = ini.ctypes.data
+    rc = lib.nvl_crc32c_fixed_host(a.ctypes.data, stride, length, n, init_ptr, init_all, out.ctypes.data,
+                                   FLAG_MASK if mask else 0)
+    check(rc, "nvl_crc32c_fixed_host")
+    return out
+
+
+def fill_splitmix(buf, nblocks: int, block_bytes: int, seed: int, *, first_block: int = 0,
+                  block_step: int = 1) -> None:
+    """Write the canonical synthetic stream into a device tensor:
+    block k <- stream bytes [(first_block + k*block_step)*block_bytes, +block_bytes)."""
+    torch = _torch()
+    _require_dev(buf, "buf", (torch.uint8, torch.int8))
+    if nblocks * block_bytes > buf.numel():
+        raise ValueError("buf too small")
+    rc = lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), nblocks, block_bytes, first_block, block_step,
+                                      seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(buf))
+    check(rc, "nvl_crc32c_fill_splitmix")
+
+
+def to_u32(t) -> np.ndarray:
+    """Device int32 result tensor -> host np.uint32 array."""
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+__all__ = ["extend", "value", "mask", "unmask", "kMaskDelta", "init", "gpu_accelerated",
+           "extend_fixed", "extend_batch", "extend_batch_host", "extend_fixed_host",
+           "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix", "to_u32", "Crc32cError"]

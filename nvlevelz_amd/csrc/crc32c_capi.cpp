@@ -1,0 +1,465 @@
+// nvlevelz_amd/csrc/crc32c_capi.cpp -- the extern "C" boundary declared in
+// include/nvl_crc32c.h.  Owns per-device lookup tables, the GPU known-answer
+// probe (util/crc32c.cc:290-297 analogue), workspace carving and the
+// host-resident staging paths.
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+#include "../../include/nvl_crc32c.h"
+#include "crc32c_internal.h"
+#include "crc32c_math.h"
+
+namespace nvl {
+
+void build_device_tables(uint32_t* w) {
+  uint32_t slice[4][256];
+  build_slice4(slice);
+  memcpy(w, slice, sizeof(slice));
+  PowTable pw;
+  build_pow_table(&pw);
+  uint32_t op[4][256];
+  for (int lev = 0; lev < 6; ++lev) {
+    build_shift_op(pw.x2n, 64ull << lev, op);
+    memcpy(w + 1024 + lev * 1024, op, sizeof(op));
+  }
+  build_shift_op(pw.x2n, 4096, op);
+  memcpy(w + 7168, op, sizeof(op));
+  memcpy(w + 8192, pw.x2n, sizeof(pw.x2n));
+}
+
+namespace {
+
+constexpr int kMaxDevices = 64;
+
+struct DeviceState {
+  int device = -1;
+  int num_cu = 0;
+  uint32_t* tables = nullptr;
+  int status = NVL_CRC32C_OK;  // OK, or why the backend is unusable
+};
+
+std::mutex g_mu;
+std::atomic<DeviceState*> g_state[kMaxDevices];
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int run_self_test(DeviceState* s);
+
+// Create (once) and return the state of `device`; nullptr on failure with *rc set.
+DeviceState* state_for(int device, int* rc) {
+  if (device < 0 || device >= kMaxDevices) {
+    *rc = NVL_CRC32C_ENODEV;
+    return nullptr;
+  }
+  DeviceState* s = g_state[device].load(std::memory_order_acquire);
+  if (s) {
+    *rc = s->status;
+    return s->status == NVL_CRC32C_OK ? s : nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  s = g_state[device].load(std::memory_order_relaxed);
+  if (!s) {
+    s = new DeviceState;
+    s->device = device;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+      s->status = NVL_CRC32C_ENODEV;
+    } else if (hipSetDevice(device) != hipSuccess ||
+               hipDeviceGetAttribute(&s->num_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+               s->num_cu <= 0) {
+      s->status = NVL_CRC32C_EHIP;
+    } else {
+      std::vector<uint32_t> words(kTableWords);
+      build_device_tables(words.data());
+      if (hipMalloc(&s->tables, kTableWords * sizeof(uint32_t)) != hipSuccess ||
+          hipMemcpy(s->tables, words.data(), kTableWords * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+        s->status = NVL_CRC32C_EHIP;
+      } else {
+        s->status = run_self_test(s);
+      }
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    g_state[device].store(s, std::memory_order_release);
+  }
+  *rc = s->status;
+  return s->status == NVL_CRC32C_OK ? s : nullptr;
+}
+
+DeviceState* current_state(int* rc) {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) {
+    *rc = NVL_CRC32C_ENODEV;
+    return nullptr;
+  }
+  return state_for(dev, rc);
+}
+
+size_t batch_ws_layout(uint64_t n, int num_cu, size_t* off_cs, size_t* off_recs, size_t* off_tmp) {
+  const size_t cnt = align_up((n + 1) * sizeof(uint64_t), 256);
+  const size_t cs = cnt;
+  const size_t recs = align_up(2ull * (size_t)num_cu * waves_per_wg() * sizeof(Rec), 256);
+  const size_t tmp = align_up(scan_temp_bytes(n + 1), 256);
+  *off_cs = cnt;
+  *off_recs = cnt + cs;
+  *off_tmp = cnt + cs + recs;
+  return cnt + cs + recs + tmp;
+}
+
+size_t fixed_ws_bytes(uint64_t len, uint64_t n, int num_cu) {
+  if (len <= 4096 || n == 0) return 0;
+  return 2ull * fixed_grid(num_cu, len, n) * waves_per_wg() * sizeof(Rec);
+}
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? NVL_CRC32C_OK : NVL_CRC32C_EHIP; }
+
+int do_fixed(DeviceState* s, const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
+             uint32_t init_all, uint32_t* out, uint32_t flags, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!out || (!base && len)) return NVL_CRC32C_EINVAL;
+  if (n > (1ull << 40) || len > (1ull << 40) || (n > 1 && stride > (1ull << 50))) return NVL_CRC32C_EINVAL;
+  const size_t need = fixed_ws_bytes(len, n, s->num_cu);
+  bool own = false;
+  if (need && !ws) {
+    if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
+    own = true;
+  } else if (need && ws_bytes < need) {
+    return NVL_CRC32C_ENOSPC;
+  }
+  LaunchCtx lc{st, s->num_cu, s->tables};
+  hipError_t e = launch_fixed(lc, static_cast<const uint8_t*>(base), stride, len, n, init, init_all, out, flags,
+                              static_cast<Rec*>(ws));
+  if (own) (void)hipFreeAsync(ws, st);
+  return hip_rc(e);
+}
+
+int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const uint64_t* lengths,
+             const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags, void* ws,
+             size_t ws_bytes, hipStream_t st) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!offsets || !lengths || !out) return NVL_CRC32C_EINVAL;
+  if (n >= (1ull << 31) - 2) return NVL_CRC32C_EINVAL;
+  size_t off_cs, off_recs, off_tmp;
+  const size_t need = batch_ws_layout(n, s->num_cu, &off_cs, &off_recs, &off_tmp);
+  bool own = false;
+  if (!ws) {
+    if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
+    own = true;
+  } else if (ws_bytes < need) {
+    return NVL_CRC32C_ENOSPC;
+  }
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint64_t* cnt = reinterpret_cast<uint64_t*>(w);
+  uint64_t* cs = reinterpret_cast<uint64_t*>(w + off_cs);
+  Rec* recs = reinterpret_cast<Rec*>(w + off_recs);
+  void* tmp = w + off_tmp;
+  hipError_t e = launch_var_counts(lengths, n, cnt, st);
+  if (e == hipSuccess) e = exclusive_scan_u64(tmp, need - off_tmp, cnt, cs, n + 1, st);
+  if (e == hipSuccess) {
+    LaunchCtx lc{st, s->num_cu, s->tables};
+    e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, n, init, init_all, out, flags,
+                   recs);
+  }
+  if (own) (void)hipFreeAsync(ws, st);
+  return hip_rc(e);
+}
+
+// Known-answer probe on the GPU: "TestCRCBuffer" -> 0xdcbc59fa at every
+// alignment 0..15 through the variable-length kernel, plus fixed-stride fast
+// and general paths against the host implementation.
+int run_self_test(DeviceState* s) {
+  hipStream_t st;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
+  int rc = NVL_CRC32C_OK;
+  const size_t kBytes = 3 * 4096 + 64;
+  std::vector<uint8_t> h(kBytes);
+  uint64_t x = 0x5EEDF00Dull;
+  for (auto& b : h) {
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    b = (uint8_t)(x >> 56);
+  }
+  static const char kTest[] = "TestCRCBuffer";
+  for (int o = 0; o < 16; ++o) memcpy(h.data() + 8192 + o * 32 + o, kTest, 13);
+  uint8_t* d = nullptr;
+  uint64_t* meta = nullptr;
+  uint32_t* out = nullptr;
+  const int nvar = 16;
+  std::vector<uint64_t> hm(2 * nvar);
+  for (int o = 0; o < nvar; ++o) {
+    hm[o] = 8192 + o * 32 + o;
+    hm[nvar + o] = 13;
+  }
+  std::vector<uint32_t> ho(nvar + 4, 0);
+  if (hipMalloc(&d, kBytes) != hipSuccess || hipMalloc(&meta, hm.size() * 8) != hipSuccess ||
+      hipMalloc(&out, ho.size() * 4) != hipSuccess) {
+    rc = NVL_CRC32C_EHIP;
+  } else if (hipMemcpy(d, h.data(), kBytes, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(meta, hm.data(), hm.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = NVL_CRC32C_EHIP;
+  } else {
+    rc = do_batch(s, d, meta, meta + nvar, nullptr, 0, out, nvar, 0, nullptr, 0, st);
+    if (rc == NVL_CRC32C_OK)
+      rc = do_fixed(s, d, 4096, 4096, 2, nullptr, 0, out + nvar, 0, nullptr, 0, st);  // fast path
+    if (rc == NVL_CRC32C_OK)
+      rc = do_fixed(s, d + 3, 4100, 4100, 2, nullptr, 0x1234567u, out + nvar + 2, 0, nullptr, 0, st);  // general
+    if (rc == NVL_CRC32C_OK) rc = hip_rc(hipStreamSynchronize(st));
+    if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
+    if (rc == NVL_CRC32C_OK) {
+      std::vector<uint32_t> want(ho.size());
+      for (int o = 0; o < nvar; ++o) want[o] = 0xdcbc59fau;
+      for (int k = 0; k < 2; ++k) {
+        want[nvar + k] = host_extend(0, h.data() + 4096 * k, 4096);
+        want[nvar + 2 + k] = host_extend(0x1234567u, h.data() + 3 + 4100 * k, 4100);
+      }
+      for (size_t k = 0; k < ho.size(); ++k) {
+        if (ho[k] != want[k]) {
+          rc = NVL_CRC32C_ESELFTEST;
+          fprintf(stderr, "[nvl_crc32c] self-test case %zu: gpu 0x%08x want 0x%08x\n", k, ho[k], want[k]);
+        }
+      }
+      // Debug escape hatch for kernel development only: report but do not disable.
+      const char* skip = getenv("NVL_CRC32C_SELFTEST_REPORT_ONLY");
+      if (rc == NVL_CRC32C_ESELFTEST && skip && skip[0] == '1') rc = NVL_CRC32C_OK;
+    }
+  }
+  if (d) (void)hipFree(d);
+  if (meta) (void)hipFree(meta);
+  if (out) (void)hipFree(out);
+  (void)hipStreamDestroy(st);
+  return rc;
+}
+
+// Pinned host staging for the host-resident entry points (grown on demand,
+// one per thread so concurrent callers never share it).
+struct Staging {
+  void* host = nullptr;
+  size_t host_bytes = 0;
+  ~Staging() {
+    if (host) (void)hipHostFree(host);
+  }
+  void* get(size_t bytes) {
+    if (bytes > host_bytes) {
+      if (host) (void)hipHostFree(host);
+      host = nullptr;
+      host_bytes = 0;
+      if (hipHostMalloc(&host, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+      host_bytes = bytes;
+    }
+    return host;
+  }
+};
+thread_local Staging t_staging;
+
+}  // namespace
+}  // namespace nvl
+
+using namespace nvl;
+
+extern "C" {
+
+int nvl_crc32c_abi_version(void) { return NVL_CRC32C_ABI_VERSION; }
+
+const char* nvl_crc32c_strerror(int status) {
+  switch (status) {
+    case NVL_CRC32C_OK: return "ok";
+    case NVL_CRC32C_EINVAL: return "invalid argument";
+    case NVL_CRC32C_EHIP: return "HIP runtime error";
+    case NVL_CRC32C_ENODEV: return "no HIP device";
+    case NVL_CRC32C_ESELFTEST: return "GPU CRC32C backend failed its known-answer self-test";
+    case NVL_CRC32C_ENOSPC: return "workspace too small";
+    default: return "unknown status";
+  }
+}
+
+int nvl_crc32c_init(int device) {
+  int rc = NVL_CRC32C_OK;
+  state_for(device, &rc);
+  return rc;
+}
+
+int nvl_crc32c_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int d = 0; d < kMaxDevices; ++d) {
+    DeviceState* s = g_state[d].exchange(nullptr);
+    if (s) {
+      if (s->tables) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(d);
+        (void)hipFree(s->tables);
+        if (prev >= 0) (void)hipSetDevice(prev);
+      }
+      delete s;
+    }
+  }
+  return NVL_CRC32C_OK;
+}
+
+int nvl_crc32c_gpu_accelerated(void) {
+  int rc = NVL_CRC32C_OK;
+  return current_state(&rc) != nullptr ? 1 : 0;
+}
+
+uint32_t nvl_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
+  return host_extend(init_crc, data, n);
+}
+
+uint32_t nvl_crc32c_value(const void* data, size_t n) { return host_extend(0, data, n); }
+
+uint32_t nvl_crc32c_mask(uint32_t crc) { return nvl::mask(crc); }
+
+uint32_t nvl_crc32c_unmask(uint32_t masked_crc) { return nvl::unmask(masked_crc); }
+
+size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, uint64_t n) {
+  (void)stride;
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  return fixed_ws_bytes(len, n, s ? s->num_cu : 256);
+}
+
+size_t nvl_crc32c_batch_workspace_bytes(uint64_t n) {
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  size_t a, b, c;
+  return batch_ws_layout(n, s ? s->num_cu : 256, &a, &b, &c);
+}
+
+int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
+                         uint32_t init_all, uint32_t* out, uint32_t flags, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  if (!s) return rc;
+  return do_fixed(s, base, stride, len, n, init, init_all, out, flags, workspace, workspace_bytes,
+                  static_cast<hipStream_t>(stream));
+}
+
+int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64_t* lengths, const uint32_t* init,
+                         uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  if (!s) return rc;
+  return do_batch(s, base, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
+                  static_cast<hipStream_t>(stream));
+}
+
+int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, const uint32_t* init,
+                          uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!ptrs || !lengths || !out) return NVL_CRC32C_EINVAL;
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  if (!s) return rc;
+  // host layout: [data (16-B aligned per buffer)] [offsets n] [lengths n] [init n]
+  uint64_t data_bytes = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!ptrs[i] && lengths[i]) return NVL_CRC32C_EINVAL;
+    data_bytes += align_up(lengths[i], 16);
+  }
+  const size_t meta_off = align_up(data_bytes, 256);
+  const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
+  uint8_t* hst = static_cast<uint8_t*>(t_staging.get(total));
+  if (!hst) return NVL_CRC32C_EHIP;
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(hst + meta_off);
+  uint64_t* hlen = hoff + n;
+  uint32_t* hini = reinterpret_cast<uint32_t*>(hlen + n);
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (lengths[i]) memcpy(hst + pos, ptrs[i], lengths[i]);
+    hoff[i] = pos;
+    hlen[i] = lengths[i];
+    hini[i] = init ? init[i] : init_all;
+    pos += align_up(lengths[i], 16);
+  }
+  hipStream_t st;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
+  uint8_t* d = nullptr;
+  size_t off_cs, off_recs, off_tmp;
+  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_recs, &off_tmp);
+  const size_t dbytes = total + n * 4 + ws + 512;
+  if (hipMallocAsync(&d, dbytes, st) != hipSuccess) {
+    (void)hipStreamDestroy(st);
+    return NVL_CRC32C_EHIP;
+  }
+  uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
+  void* dws = d + align_up(total, 256) + align_up(n * 4, 256);
+  hipError_t e = hipMemcpyAsync(d, hst, total, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
+                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);
+  else
+    rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
+  (void)hipFreeAsync(d, st);
+  if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  (void)hipStreamDestroy(st);
+  return rc;
+}
+
+int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
+                          uint32_t init_all, uint32_t* out, uint32_t flags) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!base || !out) return NVL_CRC32C_EINVAL;
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  if (!s) return rc;
+  // Slabs of whole buffers, ~64 MiB each, double-buffered over two streams:
+  // H2D(k+1) overlaps kernel(k) and D2H(k-1).
+  const uint64_t span = stride;  // bytes between buffer starts
+  uint64_t per = span ? std::max<uint64_t>(1, (64ull << 20) / std::max<uint64_t>(span, 1)) : n;
+  per = std::min<uint64_t>(per, n);
+  const uint64_t slab_bytes = (per - 1) * stride + len;
+  const size_t ws = fixed_ws_bytes(len, per, s->num_cu);
+  hipStream_t st[2];
+  uint8_t* dbuf[2] = {nullptr, nullptr};
+  uint32_t* dout[2] = {nullptr, nullptr};
+  uint32_t* dini[2] = {nullptr, nullptr};
+  void* dws[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; ++k) {
+    if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
+    if (hipMalloc(&dbuf[k], align_up(slab_bytes, 256) + per * 8 + ws + 512) != hipSuccess) rc = NVL_CRC32C_EHIP;
+    else {
+      dout[k] = reinterpret_cast<uint32_t*>(dbuf[k] + align_up(slab_bytes, 256));
+      dini[k] = dout[k] + per;
+      dws[k] = reinterpret_cast<uint8_t*>(dini[k] + per) + 256 - ((uintptr_t)(dini[k] + per) & 255);
+    }
+  }
+  const uint8_t* hb = static_cast<const uint8_t*>(base);
+  for (uint64_t i0 = 0, k = 0; rc == NVL_CRC32C_OK && i0 < n; i0 += per, k ^= 1) {
+    const uint64_t m = std::min<uint64_t>(per, n - i0);
+    const uint64_t bytes = (m - 1) * stride + len;
+    hipError_t e = hipMemcpyAsync(dbuf[k], hb + i0 * stride, bytes, hipMemcpyHostToDevice, st[k]);
+    if (e == hipSuccess && init) e = hipMemcpyAsync(dini[k], init + i0, m * 4, hipMemcpyHostToDevice, st[k]);
+    if (e != hipSuccess) { rc = NVL_CRC32C_EHIP; break; }
+    rc = do_fixed(s, dbuf[k], stride, len, m, init ? dini[k] : nullptr, init_all, dout[k], flags, dws[k], ws,
+                  st[k]);
+    if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out + i0, dout[k], m * 4, hipMemcpyDeviceToHost, st[k]));
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (hipStreamSynchronize(st[k]) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+    if (dbuf[k]) (void)hipFree(dbuf[k]);
+    (void)hipStreamDestroy(st[k]);
+  }
+  return rc;
+}
+
+int nvl_crc32c_fill_splitmix(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block,
+                             uint64_t block_step, uint64_t seed, void* stream) {
+  if (nblocks == 0) return NVL_CRC32C_OK;
+  if (!dst || block_bytes == 0 || (block_bytes % 8) != 0) return NVL_CRC32C_EINVAL;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return NVL_CRC32C_ENODEV;
+  return hip_rc(launch_fill(dst, nblocks, block_bytes, first_block, block_step, seed,
+                            static_cast<hipStream_t>(stream)));
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// nvlevelz_amd/csrc/crc32c_internal.h -- internal interfaces between the
+// C-ABI layer (crc32c_capi.cpp) and the kernel launchers (crc32c_kernels.hip,
+// crc32c_scan.hip).  Not installed; not part of the ABI.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace nvl {
+
+// Device table blob (u32 words), built on the host by build_device_tables():
+//   [0,     1024)  slice4[4][256]     util/crc32c.cc:18-281 equivalents
+//   [1024,  7168)  comb[6][4][256]    shift by 64*2^k bytes, byte-sliced
+//   [7168,  8192)  sh4096[4][256]     shift by 4096 bytes, byte-sliced
+//   [8192,  8256)  x2n[64]            x^(2^k) mod P
+constexpr uint32_t kTableWords = 8256;
+
+// A portion of one buffer processed by one wave (fix-up input).
+struct Rec {
+  unsigned long long buf;  // buffer index, kNoBuf when unused
+  uint32_t raw;            // raw register of the portion (ends at the portion end)
+  uint32_t cnt;            // chunks in the portion | kRecEnds if it holds the last chunk
+};
+constexpr unsigned long long kNoBuf = ~0ull;
+constexpr uint32_t kRecEnds = 0x80000000u;
+
+struct LaunchCtx {
+  hipStream_t stream;
+  int num_cu;
+  const uint32_t* tables;  // device blob
+};
+
+void build_device_tables(uint32_t* words /* kTableWords */);
+
+hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
+                        const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs);
+uint32_t fixed_grid(int num_cu, uint64_t len, uint64_t n);
+uint32_t waves_per_wg();
+
+hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st);
+hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
+                      const uint64_t* chunk_start, uint64_t n, const uint32_t* init, uint32_t init_all,
+                      uint32_t* out, uint32_t flags, Rec* recs);
+
+hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
+                       uint64_t seed, hipStream_t st);
+
+// Exclusive prefix sum over n u64 (crc32c_scan.hip, hipCUB).
+size_t scan_temp_bytes(uint64_t n);
+hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
+                              hipStream_t st);
+
+// CPU single-buffer Extend (crc32c_host.cpp).
+uint32_t host_extend(uint32_t init, const void* data, size_t n);
+
+}  // namespace nvl

@@ -1,0 +1,550 @@
+// nvlevelz_amd/csrc/crc32c_kernels.hip -- CDNA4 (gfx950) batched CRC32C.
+//
+// Replaces the per-call hot loops of the reference,
+//   port/port_posix_sse.cc:103-105  (8 B crc32q steps)  and
+//   util/crc32c.cc:333-339          (slice-by-4 STEP4),
+// with a batched, device-resident engine.  Bit-exact with
+// leveldb::crc32c::Extend (util/crc32c.cc:299-347).
+//
+// Work decomposition:
+//   * A buffer of L bytes is cut into J = max(1, ceil(L/4096)) "chunks",
+//     END-aligned: chunk c covers [e - 4096*(J-c), e - 4096*(J-1-c)) ∩ [p, e)
+//     for buffer [p, e).  Only chunk 0 (the head) can be short.
+//   * One wavefront processes one chunk: lane l owns the contiguous 64-byte
+//     "piece" [ce - 64*(64-l), ce - 64*(63-l)) of the chunk ending at ce, loads
+//     it with four (five when misaligned) 16-byte global loads, and runs a
+//     serial slice-by-4 over its 16 words.  Bytes before the buffer start are
+//     zero (leading zeros do not change a zero-state register), and the
+//     buffer's ~init is XORed into its first four bytes
+//     (raw(s, w||rest) = raw(0, (w^s)||rest)), so every piece starts from 0.
+//   * The 64 per-lane registers are folded with a 6-level butterfly:
+//     level k combines neighbouring groups of 2^k pieces with the GF(2)
+//     operator "shift by 64*2^k bytes", applied as 4 byte-table lookups that
+//     are spread over the group's lanes and XOR-reduced with DPP.
+//   * A wave walks a contiguous range of chunk indices; consecutive chunks of
+//     one buffer accumulate as acc = shift4096(acc) ^ raw.  A buffer whose
+//     chunks span several waves leaves per-wave records that a small fix-up
+//     kernel folds (shift by 4096*k bytes, k the later waves' chunk count).
+//
+// Lookup tables live in LDS.  The four slice-by-4 tables are replicated 32
+// times with the replica chosen by lane%32, so a wave's ds_read_b32 of
+// data-dependent indices never bank-conflicts (bank = lane%32).  Address of
+// table t, byte b, lane l:  (t>>1)<<16 | b<<8 | (t&1)<<7 | (l&31)<<2, formed
+// with ONE v_perm_b32 per lookup from the data word and a per-lane base.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_internal.h"
+#include "crc32c_math.h"
+
+namespace nvl {
+namespace dev {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 16;
+constexpr int kThreads = kWave * kWavesPerWG;  // 1024
+constexpr uint32_t kChunk = 4096;
+
+// LDS image (bytes)
+constexpr uint32_t kRepBytes = 128u * 1024u;           // 4 tables x 256 x 32 replicas x 4 B
+constexpr uint32_t kCombOff = kRepBytes;               // comb[6][4][256] u32
+constexpr uint32_t kShOff = kCombOff + 6u * 4u * 256u * 4u;
+constexpr uint32_t kLdsBytes = kShOff + 4u * 256u * 4u;  // 159744 B
+static_assert(kLdsBytes <= 160u * 1024u, "LDS image exceeds 160 KiB");
+
+// DevTables word offsets (see crc32c_internal.h)
+constexpr uint32_t kGSlice = 0, kGComb = 1024, kGX2n = 1024 + 6144 + 1024;  // sh4096 at 7168 follows comb
+
+// ---------------------------------------------------------------------------
+// cross-lane helpers (all called with EXEC = all 64 lanes)
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t swz_xor4(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);  // and 0x1f, xor 4
+}
+__device__ __forceinline__ uint32_t dpp_xor8(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);  // row_ror:8
+}
+__device__ __forceinline__ uint32_t swz_xor16(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);  // and 0x1f, xor 16
+}
+__device__ __forceinline__ uint32_t xor32(uint32_t v) {
+  return (uint32_t)__shfl_xor((int)v, 32);
+}
+
+template <int LEV>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (LEV == 0) return dpp_xor1(v);
+  else if constexpr (LEV == 1) return dpp_xor2(v);
+  else if constexpr (LEV == 2) return swz_xor4(v);
+  else if constexpr (LEV == 3) return dpp_xor8(v);
+  else if constexpr (LEV == 4) return swz_xor16(v);
+  else return xor32(v);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+typedef const u32x4 __attribute__((address_space(1))) * gvec_ptr;
+
+// 16-byte streaming load from global memory (read-once data: non-temporal
+// hint).  The explicit address space keeps it a global_load (a flat_load would
+// also count in lgkmcnt and serialise against the LDS lookups).
+__device__ __forceinline__ u32x4 ld16(uintptr_t addr) {
+  return __builtin_nontemporal_load((gvec_ptr)addr);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t* lds, uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(lds + off);
+}
+
+// Per-lane replica bases for slice tables t = 3, 2, 1, 0.
+struct LaneBase {
+  uint32_t t3, t2, t1, t0;
+};
+
+__device__ __forceinline__ LaneBase make_lane_base(int lane) {
+  const uint32_t r = (uint32_t)(lane & 31) << 2;
+  return LaneBase{(1u << 16) | 0x80u | r, (1u << 16) | r, 0x80u | r, r};
+}
+
+// One slice-by-4 step (util/crc32c.cc:287-289 STEP4 semantics): x = crc ^ word,
+// result = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].
+__device__ __forceinline__ uint32_t slice4(const uint8_t* lds, uint32_t x, const LaneBase& lb) {
+  const uint32_t a0 = __builtin_amdgcn_perm(x, lb.t3, 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, lb.t2, 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, lb.t1, 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, lb.t0, 0x0C020700u);
+  return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
+}
+
+__device__ __forceinline__ uint32_t comb_lookup(const uint8_t* lds, int lev, int j, uint32_t v) {
+  return lds_u32(lds, kCombOff + ((uint32_t)((lev * 4 + j) << 8) + ((v >> (8 * j)) & 0xFFu)) * 4u);
+}
+
+template <int LEV>
+__device__ __forceinline__ uint32_t fold_level(const uint8_t* lds, uint32_t g, int lane) {
+  const uint32_t pt = lane_xor<LEV>(g);
+  const bool hi = (lane >> LEV) & 1;
+  const uint32_t left = hi ? pt : g;
+  const uint32_t right = hi ? g : pt;
+  uint32_t s;
+  if constexpr (LEV == 0) {
+    const int j = hi ? 2 : 0;
+    s = comb_lookup(lds, 0, j, left) ^ comb_lookup(lds, 0, j + 1, left);
+    s ^= dpp_xor1(s);
+  } else {
+    s = comb_lookup(lds, LEV, lane & 3, left);
+    s ^= dpp_xor1(s);
+    s ^= dpp_xor2(s);
+  }
+  return s ^ right;
+}
+
+// XOR_l shift(g_l, 64*(63-l)) over the wave; every lane gets the result.
+__device__ __forceinline__ uint32_t wave_fold(const uint8_t* lds, uint32_t g, int lane) {
+  g = fold_level<0>(lds, g, lane);
+  g = fold_level<1>(lds, g, lane);
+  g = fold_level<2>(lds, g, lane);
+  g = fold_level<3>(lds, g, lane);
+  g = fold_level<4>(lds, g, lane);
+  g = fold_level<5>(lds, g, lane);
+  return g;
+}
+
+// shift(acc, 4096) for a wave-uniform acc; every lane gets the result.
+__device__ __forceinline__ uint32_t shift4096(const uint8_t* lds, uint32_t acc, int lane) {
+  const int j = lane & 3;
+  uint32_t s = lds_u32(lds, kShOff + ((uint32_t)(j << 8) + ((acc >> (8 * j)) & 0xFFu)) * 4u);
+  s ^= dpp_xor1(s);
+  s ^= dpp_xor2(s);
+  return s;
+}
+
+// Fill the LDS image from the device table blob.
+__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restrict__ g) {
+  const int t = threadIdx.x;
+  // replicated slice tables: 8192 16-byte stores, consecutive lanes write
+  // consecutive 16 B (conflict-free ds_write_b128).
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t s = (uint32_t)(t + q * kThreads);  // 16-byte slot index
+    const uint32_t off = s << 4;
+    const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
+    const uint32_t b = (off >> 8) & 0xFFu;
+    const uint32_t v = g[kGSlice + tab * 256u + b];
+    *reinterpret_cast<uint4*>(lds + off) = make_uint4(v, v, v, v);
+  }
+  // comb + sh4096 copied verbatim (7168 words = 1792 uint4)
+  const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
+  uint4* dst = reinterpret_cast<uint4*>(lds + kCombOff);
+  for (int q = t; q < 1792; q += kThreads) dst[q] = src[q];
+}
+
+__device__ __forceinline__ uint32_t finish(uint32_t crc, uint32_t flags) {
+  return (flags & 1u) ? nvl::mask(crc) : crc;
+}
+
+// Buffer geometry as seen by a wave.
+struct BufInfo {
+  const uint8_t* p;  // first byte
+  uint64_t len;      // bytes
+  uint32_t J;        // chunks
+  uint32_t s;        // ~init, injected into the first 4 bytes
+};
+
+struct FixedGeom {
+  const uint8_t* base;
+  uint64_t stride, len, n;
+  uint32_t J;
+  const uint32_t* init;
+  uint32_t init_all;
+  __device__ __forceinline__ uint64_t total() const { return n * (uint64_t)J; }
+  __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
+    i = t / J;
+    c = (uint32_t)(t - i * J);
+  }
+  __device__ __forceinline__ BufInfo info(uint64_t i) const {
+    const uint32_t ini = init ? init[i] : init_all;
+    return BufInfo{base + i * stride, len, J, ~ini};
+  }
+};
+
+struct VarGeom {
+  const uint8_t* base;
+  const uint64_t* offsets;
+  const uint64_t* lengths;
+  const uint64_t* chunk_start;  // n+1 entries, exclusive prefix of J_i
+  uint64_t n;
+  const uint32_t* init;
+  uint32_t init_all;
+  __device__ __forceinline__ uint64_t total() const { return chunk_start[n]; }
+  __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
+    uint64_t lo = 0, hi = n;  // invariant: chunk_start[lo] <= t < chunk_start[hi]
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (chunk_start[mid] <= t) lo = mid; else hi = mid;
+    }
+    i = lo;
+    c = (uint32_t)(t - chunk_start[lo]);
+  }
+  __device__ __forceinline__ BufInfo info(uint64_t i) const {
+    const uint64_t L = lengths[i];
+    const uint32_t J = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
+    const uint32_t ini = init ? init[i] : init_all;
+    return BufInfo{base + offsets[i], L, J, ~ini};
+  }
+};
+
+// Loaded bytes of one lane's piece (20 dwords covers a misaligned piece).
+struct Piece {
+  uint32_t d[20];
+};
+
+template <bool kFast>
+__device__ __forceinline__ void load_piece(const BufInfo& bi, uint32_t c, int lane, Piece& pc) {
+  const uintptr_t ce = (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
+  const uintptr_t ps = ce - (uintptr_t)(64 * (64 - lane));
+  if constexpr (kFast) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4 v = ld16(ps + 16u * (uint32_t)j);
+      pc.d[4 * j + 0] = v.x; pc.d[4 * j + 1] = v.y; pc.d[4 * j + 2] = v.z; pc.d[4 * j + 3] = v.w;
+    }
+  } else {
+    if (bi.len < 4) return;  // tiny path reads its own bytes
+    const uint32_t m = (uint32_t)(ce & 15u);
+    const uintptr_t a = ps - m;
+    const uintptr_t p = (uintptr_t)bi.p;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const bool ok = (j < 4 || m != 0) && (a + 16u * (uint32_t)j + 16u > p);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ok) v = ld16(a + 16u * (uint32_t)j);
+      pc.d[4 * j + 0] = v.x; pc.d[4 * j + 1] = v.y; pc.d[4 * j + 2] = v.z; pc.d[4 * j + 3] = v.w;
+    }
+  }
+}
+
+template <int Q0>
+__device__ __forceinline__ void realign(const Piece& pc, uint32_t r, uint32_t (&w)[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(pc.d[Q0 + k + 1], pc.d[Q0 + k], r);
+}
+
+// Raw (zero-state, ~init injected) register of the chunk, wave-uniform.
+template <bool kFast>
+__device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo& bi,
+                                              uint32_t c, int lane, const Piece& pc) {
+  uint32_t w[16];
+  if constexpr (kFast) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = pc.d[k];
+    if (c == 0 && lane == 0) w[0] ^= bi.s;
+  } else {
+    const uintptr_t ce = (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
+    const uint32_t m = (uint32_t)(ce & 15u);
+    const uint32_t r = m & 3u;
+    switch (m >> 2) {
+      case 0: realign<0>(pc, r, w); break;
+      case 1: realign<1>(pc, r, w); break;
+      case 2: realign<2>(pc, r, w); break;
+      default: realign<3>(pc, r, w); break;
+    }
+    const uintptr_t p = (uintptr_t)bi.p;
+    if (ce - kChunk < p + 4) {  // chunk holds the buffer head (or the tail of its ~init)
+      const uintptr_t ps = ce - (uintptr_t)(64 * (64 - lane));
+      int64_t rel = (int64_t)(p - ps);  // bytes of this piece before the buffer
+      rel = rel < -8 ? -8 : (rel > 72 ? 72 : rel);
+      const uint32_t s = bi.s;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int sh = (int)rel - 4 * k;
+        const uint32_t keep = sh <= 0 ? 0xFFFFFFFFu : (sh >= 4 ? 0u : (0xFFFFFFFFu << (8 * sh)));
+        uint32_t inj = 0;
+        if (sh >= 0 && sh < 4) inj = s << (8 * sh);
+        else if (sh < 0 && sh > -4) inj = s >> (-8 * sh);
+        w[k] = (w[k] & keep) ^ inj;
+      }
+    }
+  }
+  uint32_t crc = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) crc = slice4(lds, crc ^ w[k], lb);
+  return wave_fold(lds, crc, lane);
+}
+
+// Buffers shorter than 4 bytes: bytewise (util/crc32c.cc:287 STEP1), lane-uniform.
+__device__ __forceinline__ uint32_t tiny_crc(const uint8_t* lds, const BufInfo& bi) {
+  uint32_t l = bi.s;  // = ~init
+  for (uint32_t k = 0; k < (uint32_t)bi.len; ++k) {
+    const uint32_t b = bi.p[k];
+    l = lds_u32(lds, ((l ^ b) & 0xFFu) << 8) ^ (l >> 8);  // T0, replica 0
+  }
+  return ~l;
+}
+
+struct KArgs {
+  uint32_t* out;
+  uint32_t flags;
+  Rec* recs;  // 2 per wave: [2w] = head portion, [2w+1] = tail portion (or nullptr)
+  const uint32_t* tables;
+};
+
+template <bool kFast, class G>
+__device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  fill_lds(lds, ka.tables);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * kWavesPerWG;
+  const LaneBase lb = make_lane_base(lane);
+
+  const uint64_t T = g.total();
+  const uint64_t t0 = (uint64_t)((unsigned __int128)T * wave / nw);
+  const uint64_t t1 = (uint64_t)((unsigned __int128)T * (wave + 1) / nw);
+
+  Rec head{kNoBuf, 0u, 0u}, tail{kNoBuf, 0u, 0u};
+  if (t0 < t1) {
+    uint64_t i;
+    uint32_t c;
+    g.locate(t0, i, c);
+    BufInfo bi = g.info(i);
+    bool from_zero = (c == 0);
+    uint32_t acc = 0, cnt = 0;
+    Piece cur;
+    load_piece<kFast>(bi, c, lane, cur);
+    for (uint64_t t = t0; t < t1; ++t) {
+      // next chunk position + prefetch
+      uint64_t ni = i;
+      uint32_t nc = c + 1;
+      BufInfo nbi = bi;
+      if (nc == bi.J) {
+        ni = i + 1;
+        nc = 0;
+      }
+      Piece nxt;
+      if (t + 1 < t1) {
+        if (ni != i) nbi = g.info(ni);
+        load_piece<kFast>(nbi, nc, lane, nxt);
+      }
+      if (!kFast && bi.len < 4) {
+        const uint32_t v = tiny_crc(lds, bi);
+        if (lane == 0) ka.out[i] = finish(v, ka.flags);
+        cnt = 0;
+        from_zero = true;
+      } else {
+        const uint32_t raw = chunk_raw<kFast>(lds, lb, bi, c, lane, cur);
+        acc = cnt ? (shift4096(lds, acc, lane) ^ raw) : raw;
+        ++cnt;
+        if (c + 1 == bi.J) {
+          if (from_zero) {
+            if (lane == 0) ka.out[i] = finish(~acc, ka.flags);
+          } else {
+            head = Rec{i, acc, cnt | kRecEnds};
+          }
+          cnt = 0;
+          from_zero = true;
+        }
+      }
+      i = ni;
+      c = nc;
+      bi = nbi;
+      cur = nxt;
+    }
+    if (cnt) {
+      if (from_zero) tail = Rec{i, acc, cnt};
+      else head = Rec{i, acc, cnt};
+    }
+  }
+  if (ka.recs && lane == 0) {
+    ka.recs[2 * wave] = head;
+    ka.recs[2 * wave + 1] = tail;
+  }
+}
+
+template <bool kFast>
+__global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
+  run_waves<kFast>(g, ka);
+}
+
+__global__ __launch_bounds__(kThreads, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
+  run_waves<false>(g, ka);
+}
+
+// Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.
+__global__ void crc32c_var_counts(const uint64_t* __restrict__ lengths, uint64_t n,
+                                  uint64_t* __restrict__ cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const uint64_t L = lengths[i];
+    cnt[i] = L <= kChunk ? 1u : (L + kChunk - 1) / kChunk;
+  } else if (i == n) {
+    cnt[i] = 0;
+  }
+}
+
+// Fold the per-wave records of buffers that straddle waves.  One thread per
+// wave; the wave where a buffer ENDS walks back over earlier waves.
+__global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
+                                    const uint32_t* __restrict__ tables, uint32_t* __restrict__ out,
+                                    uint32_t flags) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nw) return;
+  const Rec h = recs[2 * w];
+  if (h.buf == kNoBuf || !(h.cnt & kRecEnds)) return;
+  const uint32_t* x2n = tables + kGX2n;
+  uint32_t total = h.raw;
+  uint64_t after = h.cnt & ~kRecEnds;  // chunks after the current portion
+  // Waves between the buffer's first and last portion either hold a middle
+  // portion (head record of this buffer) or have an empty chunk range (no
+  // records); the first portion is the tail record of an earlier wave.
+  for (int64_t x = (int64_t)w - 1; x >= 0; --x) {
+    const Rec hx = recs[2 * x];
+    if (hx.buf == h.buf) {  // a middle portion
+      total ^= nvl::shift_bytes(x2n, hx.raw, after * kChunk);
+      after += hx.cnt & ~kRecEnds;
+      continue;
+    }
+    const Rec tx = recs[2 * x + 1];
+    if (tx.buf == h.buf) {  // the first portion
+      total ^= nvl::shift_bytes(x2n, tx.raw, after * kChunk);
+      break;
+    }
+    if (hx.buf != kNoBuf || tx.buf != kNoBuf) break;  // unreachable for a consistent plan
+  }
+  out[h.buf] = finish(~total, flags);
+}
+
+// Synthetic stream: one thread per 8-byte word.
+__global__ void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t words_per_block, uint64_t nwords,
+                                     uint64_t first_block, uint64_t block_step, uint64_t seed) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+       w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = w / words_per_block;
+    const uint64_t j = (first_block + k * block_step) * words_per_block + (w - k * words_per_block);
+    uint64_t z = seed + (j + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    dst[w] = z ^ (z >> 31);
+  }
+}
+
+}  // namespace dev
+
+// ---------------------------------------------------------------------------
+// launchers (host)
+
+hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
+                       uint64_t seed, hipStream_t st) {
+  const uint64_t wpb = block_bytes / 8;
+  const uint64_t nwords = nblocks * wpb;
+  if (nwords == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((nwords + 255) / 256, 65536);
+  hipLaunchKernelGGL(dev::fill_splitmix_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                     static_cast<uint64_t*>(dst), wpb, nwords, first_block, block_step, seed);
+  return hipGetLastError();
+}
+
+static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, const uint32_t* tables,
+                                      uint32_t* out, uint32_t flags, hipStream_t st) {
+  const uint32_t tpb = 256;
+  hipLaunchKernelGGL(dev::crc32c_fixup_kernel, dim3((nw + tpb - 1) / tpb), dim3(tpb), 0, st, recs, nw,
+                     tables, out, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
+                        const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs) {
+  if (n == 0) return hipSuccess;
+  const uint32_t J = len <= dev::kChunk ? 1u : (uint32_t)((len + dev::kChunk - 1) / dev::kChunk);
+  const uint64_t T = n * (uint64_t)J;
+  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)lc.num_cu, (T + dev::kWavesPerWG - 1) / dev::kWavesPerWG);
+  if (grid == 0) grid = 1;
+  const bool fast = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
+  dev::FixedGeom g{base, stride, len, n, J, init, init_all};
+  dev::KArgs ka{out, flags, J > 1 ? recs : nullptr, lc.tables};
+  if (fast)
+    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<true>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  else
+    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<false>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || J == 1) return e;
+  return launch_fixup(recs, grid * dev::kWavesPerWG, lc.tables, out, flags, lc.stream);
+}
+
+uint32_t fixed_grid(int num_cu, uint64_t len, uint64_t n) {
+  const uint32_t J = len <= dev::kChunk ? 1u : (uint32_t)((len + dev::kChunk - 1) / dev::kChunk);
+  const uint64_t T = n * (uint64_t)J;
+  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cu, (T + dev::kWavesPerWG - 1) / dev::kWavesPerWG);
+  return grid ? grid : 1;
+}
+
+uint32_t waves_per_wg() { return dev::kWavesPerWG; }
+
+hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st) {
+  const uint32_t tpb = 256;
+  const uint64_t blocks = (n + 1 + tpb - 1) / tpb;
+  hipLaunchKernelGGL(dev::crc32c_var_counts, dim3((uint32_t)blocks), dim3(tpb), 0, st, lengths, n, cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
+                      const uint64_t* chunk_start, uint64_t n, const uint32_t* init, uint32_t init_all,
+                      uint32_t* out, uint32_t flags, Rec* recs) {
+  if (n == 0) return hipSuccess;
+  const uint32_t grid = (uint32_t)lc.num_cu;
+  dev::VarGeom g{base, offsets, lengths, chunk_start, n, init, init_all};
+  dev::KArgs ka{out, flags, recs, lc.tables};
+  hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_fixup(recs, grid * dev::kWavesPerWG, lc.tables, out, flags, lc.stream);
+}
+
+}  // namespace nvl

@@ -1,0 +1,233 @@
+"""oracle -- CPU checker for the CRC32C hot path.
+
+TEST INFRASTRUCTURE ONLY.  Imported solely by ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg.  The
+product package ``nvlevelz_amd`` never imports it.
+
+Two checkers are exposed:
+
+* :data:`port` -- ``liboracle.so``, the clean-room C restatement of
+  ``util/crc32c.cc:299-347`` (table path) and ``port/port_posix_sse.cc:69-126``
+  (SSE4.2 path), see ``oracle/crc32c_oracle.c``.
+* :func:`ref` -- ``oracle/_ref/libref_crc32c_{sse,table}.so``: the reference's
+  own sources compiled from ``/root/reference`` (``oracle/Makefile``).  Present
+  in this container and shipped prebuilt to the GPU box; absent only if never
+  built.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def build() -> None:
+    """Compile liboracle.so (and _ref/ when /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+class _Port:
+    """ctypes view of liboracle.so (the C restatement)."""
+
+    def __init__(self) -> None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        lib = ctypes.CDLL(path)
+        for name in ("oracle_crc32c_extend", "oracle_crc32c_extend_table",
+                     "oracle_crc32c_extend_sse"):
+            f = getattr(lib, name)
+            f.restype = ctypes.c_uint32
+            f.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        lib.oracle_crc32c_value.restype = ctypes.c_uint32
+        lib.oracle_crc32c_value.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        lib.oracle_crc32c_mask.restype = ctypes.c_uint32
+        lib.oracle_crc32c_mask.argtypes = [ctypes.c_uint32]
+        lib.oracle_crc32c_unmask.restype = ctypes.c_uint32
+        lib.oracle_crc32c_unmask.argtypes = [ctypes.c_uint32]
+        lib.oracle_can_accelerate.restype = ctypes.c_int
+        lib.oracle_fill_splitmix.restype = None
+        lib.oracle_fill_splitmix.argtypes = [ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_size_t]
+        lib.oracle_cfg3_lengths.restype = ctypes.c_uint64
+        lib.oracle_cfg3_lengths.argtypes = [ctypes.c_uint64, ctypes.c_uint64,
+                                            _u64p, ctypes.c_uint64]
+        lib.oracle_crc32c_fixed.restype = None
+        lib.oracle_crc32c_fixed.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        lib.oracle_crc32c_varlen.restype = None
+        lib.oracle_crc32c_varlen.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        lib.oracle_digest.restype = ctypes.c_uint32
+        lib.oracle_digest.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        lib.oracle_crc32c_fixed_mt.restype = ctypes.c_int
+        lib.oracle_crc32c_fixed_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                               ctypes.c_uint64, ctypes.c_uint64,
+                                               ctypes.c_void_p, ctypes.c_int,
+                                               ctypes.c_int]
+        self.lib = lib
+
+    # -- util/crc32c.h API -------------------------------------------------
+    def extend(self, init: int, data) -> int:
+        b = bytes(data)
+        return self.lib.oracle_crc32c_extend(init & 0xFFFFFFFF, b, len(b))
+
+    def extend_table(self, init: int, data) -> int:
+        b = bytes(data)
+        return self.lib.oracle_crc32c_extend_table(init & 0xFFFFFFFF, b, len(b))
+
+    def extend_sse(self, init: int, data) -> int:
+        b = bytes(data)
+        return self.lib.oracle_crc32c_extend_sse(init & 0xFFFFFFFF, b, len(b))
+
+    def value(self, data) -> int:
+        return self.extend(0, data)
+
+    def mask(self, crc: int) -> int:
+        return self.lib.oracle_crc32c_mask(crc & 0xFFFFFFFF)
+
+    def unmask(self, m: int) -> int:
+        return self.lib.oracle_crc32c_unmask(m & 0xFFFFFFFF)
+
+    # -- synthetic inputs ------------------------------------
+    def fill(self, seed: int, offset: int, n: int) -> np.ndarray:
+        out = np.empty(n, dtype=np.uint8)
+        self.lib.oracle_fill_splitmix(seed, offset, out.ctypes.data, n)
+        return out
+
+    def cfg3_lengths(self, seed: int, total: int) -> np.ndarray:
+        k = self.lib.oracle_cfg3_lengths(seed, total, None, 0)
+        lens = np.empty(k, dtype=np.uint64)
+        self.lib.oracle_cfg3_lengths(seed, total, _ptr(lens, _u64p), k)
+        return lens
+
+    # -- batches -------------------------------------------------------------
+    def fixed(self, buf: np.ndarray, stride: int, length: int, n: int,
+              init: np.ndarray | None = None) -> np.ndarray:
+        assert buf.dtype == np.uint8 and buf.flags.c_contiguous
+        if n:
+            assert (n - 1) * stride + length <= buf.size
+        out = np.empty(n, dtype=np.uint32)
+        ini = None
+        if init is not None:
+            init = np.ascontiguousarray(init, dtype=np.uint32)
+            ini = init.ctypes.data
+        self.lib.oracle_crc32c_fixed(buf.ctypes.data, stride, length, n, ini,
+                                     out.ctypes.data)
+        return out
+
+    def varlen(self, buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+               init: np.ndarray | None = None) -> np.ndarray:
+        assert buf.dtype == np.uint8 and buf.flags.c_contiguous
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        n = offsets.size
+        if n:
+            assert int((offsets + lengths).max()) <= buf.size
+        out = np.empty(n, dtype=np.uint32)
+        ini = None
+        if init is not None:
+            init = np.ascontiguousarray(init, dtype=np.uint32)
+            ini = init.ctypes.data
+        self.lib.oracle_crc32c_varlen(buf.ctypes.data, offsets.ctypes.data,
+                                      lengths.ctypes.data, n, ini, out.ctypes.data)
+        return out
+
+    def digest(self, crcs: np.ndarray) -> int:
+        crcs = np.ascontiguousarray(crcs, dtype=np.uint32)
+        return self.lib.oracle_digest(crcs.ctypes.data, crcs.size)
+
+    def fixed_mt(self, buf: np.ndarray, stride: int, length: int, n: int,
+                 threads: int, table: bool = False) -> np.ndarray:
+        out = np.empty(n, dtype=np.uint32)
+        rc = self.lib.oracle_crc32c_fixed_mt(buf.ctypes.data, stride, length, n,
+                                             out.ctypes.data, threads, int(table))
+        if rc != 0:
+            raise RuntimeError("oracle_crc32c_fixed_mt failed")
+        return out
+
+
+class _Ref:
+    """ctypes view of a reference-built library in oracle/_ref/."""
+
+    def __init__(self, flavour: str) -> None:
+        path = os.path.join(HERE, "_ref", f"libref_crc32c_{flavour}.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL)
+        lib.ref_crc32c_extend.restype = ctypes.c_uint32
+        lib.ref_crc32c_extend.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        lib.ref_crc32c_value.restype = ctypes.c_uint32
+        lib.ref_crc32c_value.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        lib.ref_crc32c_mask.restype = ctypes.c_uint32
+        lib.ref_crc32c_mask.argtypes = [ctypes.c_uint32]
+        lib.ref_crc32c_unmask.restype = ctypes.c_uint32
+        lib.ref_crc32c_unmask.argtypes = [ctypes.c_uint32]
+        lib.ref_accelerated_crc32c.restype = ctypes.c_uint32
+        lib.ref_accelerated_crc32c.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        lib.ref_crc32c_fixed_mt.restype = ctypes.c_int
+        lib.ref_crc32c_fixed_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_int]
+        self.lib = lib
+        self.path = path
+
+    def extend(self, init: int, data) -> int:
+        b = bytes(data)
+        return self.lib.ref_crc32c_extend(init & 0xFFFFFFFF, b, len(b))
+
+    def extend_at(self, init: int, buf: np.ndarray, off: int, n: int) -> int:
+        """Extend over buf[off:off+n] in place (keeps the true alignment)."""
+        return self.lib.ref_crc32c_extend(init & 0xFFFFFFFF, buf.ctypes.data + off, n)
+
+    def value(self, data) -> int:
+        return self.extend(0, data)
+
+    def mask(self, crc: int) -> int:
+        return self.lib.ref_crc32c_mask(crc & 0xFFFFFFFF)
+
+    def unmask(self, m: int) -> int:
+        return self.lib.ref_crc32c_unmask(m & 0xFFFFFFFF)
+
+    def fixed_mt(self, buf: np.ndarray, stride: int, length: int, n: int,
+                 threads: int) -> np.ndarray:
+        out = np.empty(n, dtype=np.uint32)
+        rc = self.lib.ref_crc32c_fixed_mt(buf.ctypes.data, stride, length, n,
+                                          out.ctypes.data, threads)
+        if rc != 0:
+            raise RuntimeError("ref_crc32c_fixed_mt failed")
+        return out
+
+
+_port = None
+_refs: dict = {}
+
+
+def port() -> _Port:
+    global _port
+    if _port is None:
+        _port = _Port()
+    return _port
+
+
+def ref(flavour: str = "sse") -> _Ref:
+    if flavour not in _refs:
+        _refs[flavour] = _Ref(flavour)
+    return _refs[flavour]
+
+
+def ref_available(flavour: str = "sse") -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", f"libref_crc32c_{flavour}.so"))

@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.json from the REFERENCE's own CRC32C build.
+
+TEST INFRASTRUCTURE.  Runs in the build container only (needs
+oracle/_ref/libref_crc32c_{sse,table}.so, i.e. util/crc32c.cc +
+port/port_posix_sse.cc compiled from /root/reference by oracle/Makefile).
+Every expected value below is produced by calling the reference's
+leveldb::crc32c::Extend / Value / Mask / Unmask, and cross-checked between
+the SSE4.2 build (port/port_posix_sse.cc:69-126) and the table build
+(util/crc32c.cc:305-346) before it is written.  The inputs are either the
+RFC 3720 vectors from util/crc32c_test.cc:13-65 or the canonical splitmix64
+stream of SURVEY.md §8d.
+
+    python oracle/gen_golden.py            # writes tests/golden/
+    python oracle/gen_golden.py --no-cfg4  # skip the 10 GiB config-4 pass
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import oracle  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      "tests", "golden")
+
+
+def both(fn):
+    """Evaluate fn(ref_lib) on both reference builds and require agreement."""
+    a = fn(oracle.ref("sse"))
+    b = fn(oracle.ref("table"))
+    assert a == b, (a, b)
+    return a
+
+
+def aligned_buffer(nbytes: int, align: int = 4096) -> np.ndarray:
+    raw = np.zeros(nbytes + align, dtype=np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+def kat() -> dict:
+    out = {"source": "util/crc32c_test.cc:13-65 + extra reference calls", "value": [], "extend": [],
+           "mask": []}
+
+    def add_value(name, data: bytes):
+        out["value"].append({"name": name, "hex": data.hex(),
+                             "crc": both(lambda r: r.value(data))})
+
+    add_value("rfc3720_zeros32", bytes(32))
+    add_value("rfc3720_ones32", b"\xff" * 32)
+    add_value("rfc3720_inc32", bytes(range(32)))
+    add_value("rfc3720_dec32", bytes(range(31, -1, -1)))
+    add_value("rfc3720_iscsi48", bytes([
+        0x01, 0xc0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+        0x14, 0, 0, 0, 0, 0, 0x04, 0, 0, 0, 0, 0x14, 0, 0, 0, 0x18,
+        0x28, 0, 0, 0, 0, 0, 0, 0, 0x02, 0, 0, 0, 0, 0, 0, 0]))
+    add_value("check_123456789", b"123456789")
+    add_value("empty", b"")
+    add_value("a", b"a")
+    add_value("foo", b"foo")
+    add_value("hello world", b"hello world")
+    add_value("TestCRCBuffer", b"TestCRCBuffer")
+    add_value("x4096", b"x" * 4096)  # db/db_bench.cc:729-746 input
+
+    def add_extend(init, data: bytes):
+        out["extend"].append({"init": init, "hex": data.hex(),
+                              "crc": both(lambda r: r.extend(init, data))})
+
+    add_extend(0x12345678, b"")
+    add_extend(both(lambda r: r.value(b"hello ")), b"world")
+    add_extend(0xFFFFFFFF, b"abc")
+    add_extend(0xDEADBEEF, bytes(range(256)) * 3)
+    for v in [0, 1, 0xFFFFFFFF, 0x12345678, 0xdcbc59fa, 0x80000000, 0xa282ead8]:
+        out["mask"].append({"crc": v, "masked": both(lambda r: r.mask(v)),
+                            "unmasked": both(lambda r: r.unmask(v))})
+    return out
+
+
+def sweep() -> dict:
+    """CRCs of stream bytes at every (offset 0..15, length 0..320) plus a few
+    long lengths, each evaluated at its true address alignment (offset o within
+    a 4096-aligned buffer) so both reference backends' alignment prologues are
+    exercised."""
+    seed = 0x5EED00AA
+    p = oracle.port()
+    buf = aligned_buffer(70000)
+    buf[:] = p.fill(seed, 0, buf.size)
+    lengths = list(range(0, 321)) + [511, 512, 513, 1023, 1024, 1025, 4095, 4096, 4097,
+                                     4100, 8191, 8192, 12345, 65535, 65536]
+    crcs = []
+    for o in range(16):
+        row = []
+        for n in lengths:
+            row.append(both(lambda r: r.extend_at(0, buf, o, n)))
+        crcs.append(row)
+    # Extend() with non-zero init at a handful of (offset, length) points
+    rng = np.random.default_rng(1234)
+    ext = []
+    for _ in range(200):
+        o = int(rng.integers(0, 4096))
+        n = int(rng.integers(0, 9000))
+        init = int(rng.integers(0, 2**32))
+        ext.append([o, n, init, both(lambda r: r.extend_at(init, buf, o, n))])
+    return {"seed": seed, "stream_bytes": int(buf.size), "offsets": list(range(16)),
+            "lengths": lengths, "crc": crcs, "extend": ext}
+
+
+def framing() -> dict:
+    """SSTable block trailers (table/table_builder.cc:183-188, checked by
+    table/format.cc:90-96) and log record headers (db/log_writer.cc:88-97,
+    checked by db/log_reader.cc:253-256) for synthetic contents."""
+    p = oracle.port()
+    rng = np.random.default_rng(99)
+    blocks = []
+    for i in range(12):
+        n = int(rng.integers(3363, 4109))  # data-block sizes measured in SURVEY §3A
+        data = p.fill(0x5EED00B0 + i, 0, n).tobytes()
+        btype = int(i % 2)  # kNoCompression=0, kSnappyCompression=1
+        crc = both(lambda r: r.extend(r.value(data), bytes([btype])))
+        blocks.append({"hex": data.hex(), "type": btype, "crc": crc,
+                       "masked": both(lambda r: r.mask(crc)),
+                       "check": both(lambda r: r.value(data + bytes([btype])))})
+    records = []
+    for i in range(12):
+        n = int(rng.integers(0, 32762))  # kBlockSize - kHeaderSize payload cap
+        payload = p.fill(0x5EED00C0 + i, 0, n).tobytes()
+        rtype = int(1 + i % 4)  # kFullType..kLastType
+        type_crc = both(lambda r: r.value(bytes([rtype])))
+        crc = both(lambda r: r.extend(type_crc, payload))
+        records.append({"len": n, "seed": 0x5EED00C0 + i, "type": rtype, "type_crc": type_crc,
+                        "crc": crc, "masked": both(lambda r: r.mask(crc))})
+    return {"sstable_blocks": blocks, "log_records": records}
+
+
+def configs(do_cfg4: bool) -> dict:
+    p = oracle.port()
+    r = oracle.ref("sse")
+    out = {}
+    # config 2: 1e5 x 4096, stride 4096, seed 0x5EED0001
+    n, L = 100_000, 4096
+    buf = aligned_buffer(n * L)
+    buf[:] = p.fill(0x5EED0001, 0, buf.size)
+    crc = r.fixed_mt(buf, L, L, n, 8)
+    assert crc[0] == oracle.ref("table").value(buf[:L].tobytes())
+    out["cfg2"] = {"seed": 0x5EED0001, "n": n, "len": L, "stride": L,
+                   "crc_first": [int(x) for x in crc[:8]], "crc_last": int(crc[-1]),
+                   "digest": p.digest(crc)}
+    del buf
+    # config 3: 1 GiB packed variable lengths
+    total = 1 << 30
+    lens = p.cfg3_lengths(0x5EED0003, total)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    buf = aligned_buffer(total)
+    buf[:] = p.fill(0x5EED0002, 0, total)
+    crc = np.array([r.extend_at(0, buf, int(o), int(m)) for o, m in zip(offs, lens)],
+                   dtype=np.uint32)
+    out["cfg3"] = {"seed": 0x5EED0002, "len_seed": 0x5EED0003, "total": total,
+                   "n": int(lens.size), "len_first": int(lens[0]), "len_last": int(lens[-1]),
+                   "crc_first": [int(x) for x in crc[:8]], "crc_last": int(crc[-1]),
+                   "digest": p.digest(crc)}
+    del buf
+    if do_cfg4:
+        n, L = 5000, 2 << 20
+        crc = np.empty(n, dtype=np.uint32)
+        part = aligned_buffer(L * 100)
+        for s in range(0, n, 100):
+            part[:] = p.fill(0x5EED0004, s * L, part.size)
+            crc[s:s + 100] = r.fixed_mt(part, L, L, 100, 8)
+        out["cfg4"] = {"seed": 0x5EED0004, "n": n, "len": L, "stride": L,
+                       "crc_first": [int(x) for x in crc[:8]], "crc_last": int(crc[-1]),
+                       "digest": p.digest(crc)}
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--no-cfg4", action="store_true")
+    args = ap.parse_args()
+    os.makedirs(GOLDEN, exist_ok=True)
+    provenance = {"generator": "oracle/gen_golden.py",
+                  "reference_builds": [oracle.ref("sse").path, oracle.ref("table").path]}
+    for name, fn in [("kat", kat), ("sweep", sweep), ("framing", framing)]:
+        d = fn()
+        d["provenance"] = provenance
+        with open(os.path.join(GOLDEN, f"{name}.json"), "w") as f:
+            json.dump(d, f, separators=(",", ":"))
+        print("wrote", name)
+    d = configs(not args.no_cfg4)
+    d["provenance"] = provenance
+    with open(os.path.join(GOLDEN, "configs.json"), "w") as f:
+        json.dump(d, f, indent=1)
+    print(json.dumps({k: {kk: (hex(vv) if isinstance(vv, int) and kk in ("digest", "crc_last") else vv)
+                          for kk, vv in v.items() if kk != "crc_first"}
+                      for k, v in d.items() if k.startswith("cfg")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

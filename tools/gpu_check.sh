@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, a short bench, and a rocprofv3 kernel-trace summary.
+# Usage (from the repo root on the GPU box): bash tools/gpu_check.sh TAG
+set -o pipefail
+TAG=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd $R
+echo "[gpu_check] $(date) start tag=$TAG"
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/pytest_gpu_$TAG.log 2>&1
+rc=$?; echo "[gpu_check] pytest rc=$rc"; tail -5 $OUT/pytest_gpu_$TAG.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1
+rc=$?; echo "[gpu_check] smoke rc=$rc"; tail -2 $OUT/smoke_$TAG.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --e2e > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+rc=$?; echo "[gpu_check] bench rc=$rc"; cat $OUT/bench_$TAG.json
+[ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
+  python3 $R/bench.py --no-cpu --steps 50 --warmup 5 > $OUT/prof_$TAG.log 2>&1
+rc=$?; echo "[gpu_check] rocprof rc=$rc"
+find $OUT/prof_$TAG -name '*stats*' | head
+exit $rc

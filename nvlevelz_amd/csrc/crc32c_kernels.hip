@@ -88,6 +88,12 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#if defined(NVL_ABL_STRIDED) || defined(NVL_ABL_NOLOAD)
+#define NVL_ABL_LAYOUT_STRIDED 1
+#else
+#define NVL_ABL_LAYOUT_STRIDED 0
+#endif
+
 typedef const u32x4 __attribute__((address_space(1))) * gvec_ptr;
 
 // 16-byte streaming load from global memory (read-once data: non-temporal
@@ -125,7 +131,11 @@ __device__ __forceinline__ uint32_t comb_lookup(const uint8_t* lds, int lev, int
   return lds_u32(lds, kCombOff + ((uint32_t)((lev * 4 + j) << 8) + ((v >> (8 * j)) & 0xFFu)) * 4u);
 }
 
-template <int LEV>
+// One butterfly level over lane bit LEV: the lane with bit LEV clear holds the
+// group of lower stream positions ("left"), the partner the upper one
+// ("right"); left is shifted by the operator in comb table TAB (64*2^TAB
+// bytes) and XORed in.  Lanes 0..3 of every quad spread the 4 byte lookups.
+template <int LEV, int TAB = LEV>
 __device__ __forceinline__ uint32_t fold_level(const uint8_t* lds, uint32_t g, int lane) {
   const uint32_t pt = lane_xor<LEV>(g);
   const bool hi = (lane >> LEV) & 1;
@@ -134,10 +144,10 @@ __device__ __forceinline__ uint32_t fold_level(const uint8_t* lds, uint32_t g, i
   uint32_t s;
   if constexpr (LEV == 0) {
     const int j = hi ? 2 : 0;
-    s = comb_lookup(lds, 0, j, left) ^ comb_lookup(lds, 0, j + 1, left);
+    s = comb_lookup(lds, TAB, j, left) ^ comb_lookup(lds, TAB, j + 1, left);
     s ^= dpp_xor1(s);
   } else {
-    s = comb_lookup(lds, LEV, lane & 3, left);
+    s = comb_lookup(lds, TAB, lane & 3, left);
     s ^= dpp_xor1(s);
     s ^= dpp_xor2(s);
   }
@@ -244,14 +254,52 @@ struct Piece {
   uint32_t d[20];
 };
 
+// 4x4 transpose of 16-byte slots inside each lane quad (DPP quad_perm):
+// afterwards lane 4q+r holds, in slot s, what lane 4q+s held in slot r.
+__device__ __forceinline__ void quad_transpose(int lane, uint32_t (&d)[20]) {
+  const int r = lane & 3;
+  uint32_t t[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // stage 1: swap 2x2 blocks across lane bit 1
+    const bool take = ((j >> 1) & 1) != ((r >> 1) & 1);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const uint32_t o = dpp_xor2(d[4 * (j ^ 2) + x]);
+      t[4 * j + x] = take ? o : d[4 * j + x];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // stage 2: swap within 2x2 blocks across lane bit 0
+    const bool take = (j & 1) != (r & 1);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const uint32_t o = dpp_xor1(t[4 * (j ^ 1) + x]);
+      d[4 * j + x] = take ? o : t[4 * j + x];
+    }
+  }
+}
+
+// Fast path (16-B aligned, full 4 KiB chunks): four fully coalesced 1 KiB
+// loads (row j = bytes [1024j, 1024j+1024) of the chunk, lane l at 16l).  After
+// quad_transpose (in build_words) lane 4q+r holds the contiguous 64-byte piece
+// at chunk position P = 16r + q.
 template <bool kFast>
 __device__ __forceinline__ void load_piece(const BufInfo& bi, uint32_t c, int lane, Piece& pc) {
   const uintptr_t ce = (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
   const uintptr_t ps = ce - (uintptr_t)(64 * (64 - lane));
   if constexpr (kFast) {
+#if defined(NVL_ABL_NOLOAD)  // ablation: synthetic data, no global loads
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pc.d[k] = (uint32_t)(ps >> 4) * 2654435761u + (uint32_t)k * 40503u;
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+#if defined(NVL_ABL_STRIDED)  // ablation: the v1 lane-contiguous (64-B stride) loads
       const u32x4 v = ld16(ps + 16u * (uint32_t)j);
+#else
+      const u32x4 v = ld16(ce - kChunk + 1024u * (uint32_t)j + 16u * (uint32_t)lane);
+#endif
       pc.d[4 * j + 0] = v.x; pc.d[4 * j + 1] = v.y; pc.d[4 * j + 2] = v.z; pc.d[4 * j + 3] = v.w;
     }
   } else {
@@ -275,15 +323,19 @@ __device__ __forceinline__ void realign(const Piece& pc, uint32_t r, uint32_t (&
   for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(pc.d[Q0 + k + 1], pc.d[Q0 + k], r);
 }
 
-// Raw (zero-state, ~init injected) register of the chunk, wave-uniform.
+// The 16 little-endian words of this lane's piece, realigned, with the head
+// masking and ~init injection applied (wave-uniform control flow).
 template <bool kFast>
-__device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo& bi,
-                                              uint32_t c, int lane, const Piece& pc) {
-  uint32_t w[16];
+__device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int lane, const Piece& pc,
+                                            uint32_t (&w)[16]) {
   if constexpr (kFast) {
+    Piece t = pc;
+#if !defined(NVL_ABL_STRIDED) && !defined(NVL_ABL_NOLOAD)
+    quad_transpose(lane, t.d);
+#endif
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = pc.d[k];
-    if (c == 0 && lane == 0) w[0] ^= bi.s;
+    for (int k = 0; k < 16; ++k) w[k] = t.d[k];
+    if (c == 0 && lane == 0) w[0] ^= bi.s;  // position 0 is lane 0 in both layouts
   } else {
     const uintptr_t ce = (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
     const uint32_t m = (uint32_t)(ce & 15u);
@@ -311,10 +363,66 @@ __device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase
       }
     }
   }
-  uint32_t crc = 0;
+}
+
+// Raw (zero-state, ~init injected) registers of U chunks, wave-uniform.  The
+// U serial slice-by-4 chains and U butterflies are interleaved so each wave
+// keeps U independent LDS round trips in flight (the kernel is bound by the
+// chain's LDS latency, not by LDS bandwidth).
+template <bool kFast, int U>
+__device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo (&bi)[U],
+                                          const uint32_t (&c)[U], int lane, const Piece (&pc)[U],
+                                          uint32_t (&raw)[U]) {
+  uint32_t w[U][16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) crc = slice4(lds, crc ^ w[k], lb);
-  return wave_fold(lds, crc, lane);
+  for (int u = 0; u < U; ++u) build_words<kFast>(bi[u], c[u], lane, pc[u], w[u]);
+  uint32_t crc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = 0;
+#if defined(NVL_ABL_NOCOMPUTE)  // ablation: keep the loads live, skip every lookup
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) crc[u] ^= w[u][k];
+    crc[u] ^= lane_xor<5>(crc[u]);
+    raw[u] = crc[u];
+  }
+  return;
+#endif
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) crc[u] = slice4(lds, crc[u] ^ w[u][k], lb);
+  }
+  // Lane -> stream position: general path P = lane; fast path (transposed
+  // rows) P = 16*(lane&3) + (lane>>2), so lane bits 0,1 step 1024/2048 bytes
+  // and bits 2..5 step 64..512 bytes.
+  constexpr bool kT = kFast && !NVL_ABL_LAYOUT_STRIDED;
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, kT ? 4 : 0>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, kT ? 5 : 1>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, kT ? 0 : 2>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, kT ? 1 : 3>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, kT ? 2 : 4>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, kT ? 3 : 5>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) raw[u] = crc[u];
+}
+
+template <bool kFast>
+__device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo& bi,
+                                              uint32_t c, int lane, const Piece& pc) {
+  const BufInfo b1[1] = {bi};
+  const uint32_t c1[1] = {c};
+  const Piece p1[1] = {pc};
+  uint32_t r1[1];
+  group_raw<kFast, 1>(lds, lb, b1, c1, lane, p1, r1);
+  return r1[0];
 }
 
 // Buffers shorter than 4 bytes: bytewise (util/crc32c.cc:287 STEP1), lane-uniform.
@@ -334,7 +442,49 @@ struct KArgs {
   const uint32_t* tables;
 };
 
-template <bool kFast, class G>
+// Position of one chunk inside a wave's range.
+struct Pos {
+  uint64_t i;  // buffer
+  uint32_t c;  // chunk within the buffer
+  BufInfo bi;
+};
+
+template <class G>
+__device__ __forceinline__ Pos next_pos(const G& g, const Pos& p) {
+  Pos q = p;
+  if (p.c + 1 == p.bi.J) {
+    q.i = p.i + 1;
+    q.c = 0;
+    q.bi = g.info(q.i);
+  } else {
+    q.c = p.c + 1;
+  }
+  return q;
+}
+
+// Per-wave accumulation over consecutive chunks (wave-uniform).
+struct WaveState {
+  uint32_t acc, cnt;
+  bool from_zero;
+  Rec head;
+};
+
+__device__ __forceinline__ void consume(WaveState& st, const Pos& p, uint32_t raw, const uint8_t* lds, int lane,
+                                        const KArgs& ka) {
+  st.acc = st.cnt ? (shift4096(lds, st.acc, lane) ^ raw) : raw;
+  ++st.cnt;
+  if (p.c + 1 == p.bi.J) {
+    if (st.from_zero) {
+      if (lane == 0) ka.out[p.i] = finish(~st.acc, ka.flags);
+    } else {
+      st.head = Rec{p.i, st.acc, st.cnt | kRecEnds};
+    }
+    st.cnt = 0;
+    st.from_zero = true;
+  }
+}
+
+template <bool kFast, int U, class G>
 __device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   fill_lds(lds, ka.tables);
@@ -346,75 +496,106 @@ __device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
   const LaneBase lb = make_lane_base(lane);
 
   const uint64_t T = g.total();
-  const uint64_t t0 = (uint64_t)((unsigned __int128)T * wave / nw);
-  const uint64_t t1 = (uint64_t)((unsigned __int128)T * (wave + 1) / nw);
+  const uint64_t t0 = T * wave / nw;
+  const uint64_t t1 = T * (wave + 1) / nw;
 
-  Rec head{kNoBuf, 0u, 0u}, tail{kNoBuf, 0u, 0u};
+  Rec tail{kNoBuf, 0u, 0u};
+  WaveState st{0u, 0u, true, Rec{kNoBuf, 0u, 0u}};
   if (t0 < t1) {
-    uint64_t i;
-    uint32_t c;
-    g.locate(t0, i, c);
-    BufInfo bi = g.info(i);
-    bool from_zero = (c == 0);
-    uint32_t acc = 0, cnt = 0;
-    Piece cur;
-    load_piece<kFast>(bi, c, lane, cur);
-    for (uint64_t t = t0; t < t1; ++t) {
-      // next chunk position + prefetch
-      uint64_t ni = i;
-      uint32_t nc = c + 1;
-      BufInfo nbi = bi;
-      if (nc == bi.J) {
-        ni = i + 1;
-        nc = 0;
-      }
-      Piece nxt;
-      if (t + 1 < t1) {
-        if (ni != i) nbi = g.info(ni);
-        load_piece<kFast>(nbi, nc, lane, nxt);
-      }
-      if (!kFast && bi.len < 4) {
-        const uint32_t v = tiny_crc(lds, bi);
-        if (lane == 0) ka.out[i] = finish(v, ka.flags);
-        cnt = 0;
-        from_zero = true;
-      } else {
-        const uint32_t raw = chunk_raw<kFast>(lds, lb, bi, c, lane, cur);
-        acc = cnt ? (shift4096(lds, acc, lane) ^ raw) : raw;
-        ++cnt;
-        if (c + 1 == bi.J) {
-          if (from_zero) {
-            if (lane == 0) ka.out[i] = finish(~acc, ka.flags);
-          } else {
-            head = Rec{i, acc, cnt | kRecEnds};
+    Pos p;
+    g.locate(t0, p.i, p.c);
+    p.bi = g.info(p.i);
+    st.from_zero = (p.c == 0);
+    uint64_t t = t0;
+    // ---- U chunks per step, next U prefetched while these compute ----
+    if constexpr (U > 1) {
+      if (t + U <= t1) {
+        Pos gp[U];
+        Piece cur[U];
+        gp[0] = p;
+#pragma unroll
+        for (int u = 1; u < U; ++u) gp[u] = next_pos(g, gp[u - 1]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_piece<kFast>(gp[u].bi, gp[u].c, lane, cur[u]);
+        while (true) {
+          const bool more = t + 2 * U <= t1;
+          Pos np[U];
+          Piece nxt[U];
+          if (more) {
+            np[0] = next_pos(g, gp[U - 1]);
+#pragma unroll
+            for (int u = 1; u < U; ++u) np[u] = next_pos(g, np[u - 1]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_piece<kFast>(np[u].bi, np[u].c, lane, nxt[u]);
           }
-          cnt = 0;
-          from_zero = true;
+          BufInfo bis[U];
+          uint32_t cs[U], raws[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            bis[u] = gp[u].bi;
+            cs[u] = gp[u].c;
+          }
+          group_raw<kFast, U>(lds, lb, bis, cs, lane, cur, raws);
+#pragma unroll
+          for (int u = 0; u < U; ++u) consume(st, gp[u], raws[u], lds, lane, ka);
+          t += U;
+          if (!more) break;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            gp[u] = np[u];
+            cur[u] = nxt[u];
+          }
+        }
+        p = (t < t1) ? next_pos(g, gp[U - 1]) : gp[U - 1];  // chunk t, or the last one consumed
+      }
+    }
+    // ---- remaining chunks one at a time ----
+    if (t < t1) {
+      Piece cur;
+      load_piece<kFast>(p.bi, p.c, lane, cur);
+      for (; t < t1; ++t) {
+        Pos q = p;
+        Piece nxt;
+        if (t + 1 < t1) {
+          q = next_pos(g, p);
+          load_piece<kFast>(q.bi, q.c, lane, nxt);
+        }
+        if (!kFast && p.bi.len < 4) {
+          const uint32_t v = tiny_crc(lds, p.bi);
+          if (lane == 0) ka.out[p.i] = finish(v, ka.flags);
+          st.cnt = 0;
+          st.from_zero = true;
+        } else {
+          consume(st, p, chunk_raw<kFast>(lds, lb, p.bi, p.c, lane, cur), lds, lane, ka);
+        }
+        if (t + 1 < t1) {
+          p = q;
+          cur = nxt;
         }
       }
-      i = ni;
-      c = nc;
-      bi = nbi;
-      cur = nxt;
     }
-    if (cnt) {
-      if (from_zero) tail = Rec{i, acc, cnt};
-      else head = Rec{i, acc, cnt};
+    if (st.cnt) {
+      if (st.from_zero) tail = Rec{p.i, st.acc, st.cnt};
+      else st.head = Rec{p.i, st.acc, st.cnt};
     }
   }
   if (ka.recs && lane == 0) {
-    ka.recs[2 * wave] = head;
+    ka.recs[2 * wave] = st.head;
     ka.recs[2 * wave + 1] = tail;
   }
 }
 
+#ifndef NVL_FAST_U
+#define NVL_FAST_U 2  // chunks per wave step on the fast path (tools/ab_bench.py: 2 > 1 > 4)
+#endif
+
 template <bool kFast>
 __global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
-  run_waves<kFast>(g, ka);
+  run_waves<kFast, kFast ? NVL_FAST_U : 1>(g, ka);
 }
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
-  run_waves<false>(g, ka);
+  run_waves<false, 1>(g, ka);
 }
 
 // Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.

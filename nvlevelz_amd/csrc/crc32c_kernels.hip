@@ -48,12 +48,13 @@ constexpr uint32_t kChunk = 4096;
 // LDS image (bytes)
 constexpr uint32_t kRepBytes = 128u * 1024u;           // 4 tables x 256 x 32 replicas x 4 B
 constexpr uint32_t kCombOff = kRepBytes;               // comb[6][4][256] u32
-constexpr uint32_t kShOff = kCombOff + 6u * 4u * 256u * 4u;
-constexpr uint32_t kLdsBytes = kShOff + 4u * 256u * 4u;  // 159744 B
+constexpr uint32_t kShOff = kCombOff + 6u * 4u * 256u * 4u;  // sh4096[4][256] u32
+constexpr uint32_t kCtrOff = kShOff + 4u * 256u * 4u;         // per-workgroup work counter
+constexpr uint32_t kLdsBytes = kCtrOff + 16u;                 // 159760 B
 static_assert(kLdsBytes <= 160u * 1024u, "LDS image exceeds 160 KiB");
 
 // DevTables word offsets (see crc32c_internal.h)
-constexpr uint32_t kGSlice = 0, kGComb = 1024, kGX2n = 1024 + 6144 + 1024;  // sh4096 at 7168 follows comb
+constexpr uint32_t kGSlice = 0, kGComb = 1024, kGX2n = 1024 + 6144 + 1024;  // comb, sh4096 contiguous
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers (all called with EXEC = all 64 lanes)
@@ -100,7 +101,11 @@ typedef const u32x4 __attribute__((address_space(1))) * gvec_ptr;
 // hint).  The explicit address space keeps it a global_load (a flat_load would
 // also count in lgkmcnt and serialise against the LDS lookups).
 __device__ __forceinline__ u32x4 ld16(uintptr_t addr) {
+#if defined(NVL_ABL_NO_NT)
+  return *(gvec_ptr)addr;
+#else
   return __builtin_nontemporal_load((gvec_ptr)addr);
+#endif
 }
 
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t* lds, uint32_t off) {
@@ -126,6 +131,32 @@ __device__ __forceinline__ uint32_t slice4(const uint8_t* lds, uint32_t x, const
   const uint32_t a3 = __builtin_amdgcn_perm(x, lb.t0, 0x0C020700u);
   return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
 }
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));  // gfx950: 3-input XOR via truth table 0x96
+  return d;
+}
+
+// slice4(x) ^ next, with the five-way XOR as two v_xor3_b32.
+__device__ __forceinline__ uint32_t slice4_x(const uint8_t* lds, uint32_t x, uint32_t next, const LaneBase& lb) {
+  const uint32_t a0 = __builtin_amdgcn_perm(x, lb.t3, 0x0C020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, lb.t2, 0x0C020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, lb.t1, 0x0C020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, lb.t0, 0x0C020700u);
+  return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1), lds_u32(lds, a2)), lds_u32(lds, a3), next);
+}
+
+// slice4(x) ^ next -- the chain step with the following word folded in.
+__device__ __forceinline__ uint32_t slice4_next(const uint8_t* lds, uint32_t x, uint32_t next, const LaneBase& lb) {
+#if defined(NVL_XOR3)
+  return slice4_x(lds, x, next, lb);
+#else
+  return slice4(lds, x, lb) ^ next;
+#endif
+}
+
+
 
 __device__ __forceinline__ uint32_t comb_lookup(const uint8_t* lds, int lev, int j, uint32_t v) {
   return lds_u32(lds, kCombOff + ((uint32_t)((lev * 4 + j) << 8) + ((v >> (8 * j)) & 0xFFu)) * 4u);
@@ -192,6 +223,7 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restric
   const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
   uint4* dst = reinterpret_cast<uint4*>(lds + kCombOff);
   for (int q = t; q < 1792; q += kThreads) dst[q] = src[q];
+  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = (uint32_t)kWavesPerWG;  // units 0..15 are pre-assigned
 }
 
 __device__ __forceinline__ uint32_t finish(uint32_t crc, uint32_t flags) {
@@ -377,23 +409,26 @@ __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb
 #pragma unroll
   for (int u = 0; u < U; ++u) build_words<kFast>(bi[u], c[u], lane, pc[u], w[u]);
   uint32_t crc[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = 0;
 #if defined(NVL_ABL_NOCOMPUTE)  // ablation: keep the loads live, skip every lookup
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    crc[u] = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) crc[u] ^= w[u][k];
-    crc[u] ^= lane_xor<5>(crc[u]);
-    raw[u] = crc[u];
+    raw[u] = crc[u] ^ lane_xor<5>(crc[u]);
   }
   return;
 #endif
+  {
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
+    for (int u = 0; u < U; ++u) crc[u] = w[u][0];
 #pragma unroll
-    for (int u = 0; u < U; ++u) crc[u] = slice4(lds, crc[u] ^ w[u][k], lb);
+    for (int k = 0; k < 16; ++k) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+    }
   }
+
   // Lane -> stream position: general path P = lane; fast path (transposed
   // rows) P = 16*(lane&3) + (lane>>2), so lane bits 0,1 step 1024/2048 bytes
   // and bits 2..5 step 64..512 bytes.
@@ -484,39 +519,60 @@ __device__ __forceinline__ void consume(WaveState& st, const Pos& p, uint32_t ra
   }
 }
 
+#if defined(NVL_DIAG_STAMPS)
+// Diagnostic build only: per-wave {start, after-fill, end} s_memtime stamps
+// and the XCC id, read back with nvl_diag_stamps().
+__device__ unsigned long long g_stamps[4 * 65536];
+#endif
+
 template <bool kFast, int U, class G>
-__device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  fill_lds(lds, ka.tables);
-  __syncthreads();
+__device__ __forceinline__ void run_waves(const G& g, const KArgs& ka, uint8_t* lds) {
+#if defined(NVL_DIAG_STAMPS)
+  const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
   const uint32_t nw = gridDim.x * kWavesPerWG;
-  const LaneBase lb = make_lane_base(lane);
 
   const uint64_t T = g.total();
   const uint64_t t0 = T * wave / nw;
   const uint64_t t1 = T * (wave + 1) / nw;
 
+  // Issue the first chunks' HBM loads before building the LDS tables so the
+  // table fill hides under their latency.
+  Pos p;
+  Pos gp[U];
+  Piece cur[U];
+  const bool grouped = (U > 1) && (t0 + U <= t1);
+  if (t0 < t1) {
+    g.locate(t0, p.i, p.c);
+    p.bi = g.info(p.i);
+    if (grouped) {
+      gp[0] = p;
+#pragma unroll
+      for (int u = 1; u < U; ++u) gp[u] = next_pos(g, gp[u - 1]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_piece<kFast>(gp[u].bi, gp[u].c, lane, cur[u]);
+    } else {
+      load_piece<kFast>(p.bi, p.c, lane, cur[0]);
+    }
+  }
+  fill_lds(lds, ka.tables);
+  __syncthreads();
+  const LaneBase lb = make_lane_base(lane);
+#if defined(NVL_DIAG_STAMPS)
+  const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
+
   Rec tail{kNoBuf, 0u, 0u};
   WaveState st{0u, 0u, true, Rec{kNoBuf, 0u, 0u}};
   if (t0 < t1) {
-    Pos p;
-    g.locate(t0, p.i, p.c);
-    p.bi = g.info(p.i);
     st.from_zero = (p.c == 0);
     uint64_t t = t0;
     // ---- U chunks per step, next U prefetched while these compute ----
     if constexpr (U > 1) {
-      if (t + U <= t1) {
-        Pos gp[U];
-        Piece cur[U];
-        gp[0] = p;
-#pragma unroll
-        for (int u = 1; u < U; ++u) gp[u] = next_pos(g, gp[u - 1]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) load_piece<kFast>(gp[u].bi, gp[u].c, lane, cur[u]);
+      if (grouped) {
         while (true) {
           const bool more = t + 2 * U <= t1;
           Pos np[U];
@@ -547,31 +603,28 @@ __device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
           }
         }
         p = (t < t1) ? next_pos(g, gp[U - 1]) : gp[U - 1];  // chunk t, or the last one consumed
+        if (t < t1) load_piece<kFast>(p.bi, p.c, lane, cur[0]);
       }
     }
-    // ---- remaining chunks one at a time ----
-    if (t < t1) {
-      Piece cur;
-      load_piece<kFast>(p.bi, p.c, lane, cur);
-      for (; t < t1; ++t) {
-        Pos q = p;
-        Piece nxt;
-        if (t + 1 < t1) {
-          q = next_pos(g, p);
-          load_piece<kFast>(q.bi, q.c, lane, nxt);
-        }
-        if (!kFast && p.bi.len < 4) {
-          const uint32_t v = tiny_crc(lds, p.bi);
-          if (lane == 0) ka.out[p.i] = finish(v, ka.flags);
-          st.cnt = 0;
-          st.from_zero = true;
-        } else {
-          consume(st, p, chunk_raw<kFast>(lds, lb, p.bi, p.c, lane, cur), lds, lane, ka);
-        }
-        if (t + 1 < t1) {
-          p = q;
-          cur = nxt;
-        }
+    // ---- remaining chunks one at a time (cur[0] holds chunk t) ----
+    for (; t < t1; ++t) {
+      Pos q = p;
+      Piece nxt;
+      if (t + 1 < t1) {
+        q = next_pos(g, p);
+        load_piece<kFast>(q.bi, q.c, lane, nxt);
+      }
+      if (!kFast && p.bi.len < 4) {
+        const uint32_t v = tiny_crc(lds, p.bi);
+        if (lane == 0) ka.out[p.i] = finish(v, ka.flags);
+        st.cnt = 0;
+        st.from_zero = true;
+      } else {
+        consume(st, p, chunk_raw<kFast>(lds, lb, p.bi, p.c, lane, cur[0]), lds, lane, ka);
+      }
+      if (t + 1 < t1) {
+        p = q;
+        cur[0] = nxt;
       }
     }
     if (st.cnt) {
@@ -583,6 +636,116 @@ __device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
     ka.recs[2 * wave] = st.head;
     ka.recs[2 * wave + 1] = tail;
   }
+#if defined(NVL_DIAG_STAMPS)
+  if (lane == 0 && wave < 65536) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_stamps[4 * wave + 0] = ts0;
+    g_stamps[4 * wave + 1] = ts1;
+    g_stamps[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+    g_stamps[4 * wave + 3] = ((unsigned long long)xcc << 32) | (t1 - t0);
+  }
+#endif
+}
+
+// Fixed stride with J == 1 (every chunk is a whole buffer; config 2): the
+// workgroup owns a contiguous range of buffers and its 16 waves pull units of
+// U buffers from an LDS counter, so fast and slow waves of a CU finish
+// together (a static per-wave split left the last wave ~20% behind the mean).
+template <int U>
+__device__ __forceinline__ void run_dynamic(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
+#if defined(NVL_DIAG_STAMPS)
+  const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t nproc = 0;
+#endif
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t B0 = g.n * blockIdx.x / gridDim.x;
+  const uint64_t B1 = g.n * (blockIdx.x + 1) / gridDim.x;
+  const uint32_t nunits = (uint32_t)((B1 - B0 + U - 1) / U);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kCtrOff);
+
+  auto unit_pos = [&](uint32_t u, int k, Pos& p) -> bool {
+    const uint64_t i = B0 + (uint64_t)u * U + (uint64_t)k;
+    if (u >= nunits || i >= B1) return false;
+    p.i = i;
+    p.c = 0;
+    p.bi = g.info(i);
+    return true;
+  };
+
+  uint32_t u = wv;  // first unit pre-assigned; its loads overlap the LDS fill
+  Pos gp[U];
+  bool ok[U];
+  Piece cur[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    ok[k] = unit_pos(u, k, gp[k]);
+    if (ok[k]) load_piece<true>(gp[k].bi, 0, lane, cur[k]);
+  }
+  fill_lds(lds, ka.tables);
+  __syncthreads();
+  const LaneBase lb = make_lane_base(lane);
+#if defined(NVL_DIAG_STAMPS)
+  const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  while (u < nunits) {
+#if defined(NVL_DIAG_STAMPS)
+    ++nproc;
+#endif
+    uint32_t un = 0;
+    if (lane == 0) un = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    un = __builtin_amdgcn_readfirstlane(un);
+    Pos np[U];
+    bool nok[U];
+    Piece nxt[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      nok[k] = unit_pos(un, k, np[k]);
+      if (nok[k]) load_piece<true>(np[k].bi, 0, lane, nxt[k]);
+    }
+    if (ok[U - 1]) {  // full unit
+      BufInfo bis[U];
+      uint32_t cs[U], raws[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        bis[k] = gp[k].bi;
+        cs[k] = 0;
+      }
+      group_raw<true, U>(lds, lb, bis, cs, lane, cur, raws);
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) ka.out[gp[k].i] = finish(~raws[k], ka.flags);
+      }
+    } else {  // the range's ragged last unit
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (ok[k]) {
+          const uint32_t r = chunk_raw<true>(lds, lb, gp[k].bi, 0, lane, cur[k]);
+          if (lane == 0) ka.out[gp[k].i] = finish(~r, ka.flags);
+        }
+      }
+    }
+    u = un;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      gp[k] = np[k];
+      ok[k] = nok[k];
+      cur[k] = nxt[k];
+    }
+  }
+#if defined(NVL_DIAG_STAMPS)
+  const uint32_t wave = blockIdx.x * kWavesPerWG + wv;
+  if (lane == 0 && wave < 65536) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_stamps[4 * wave + 0] = ts0;
+    g_stamps[4 * wave + 1] = ts1;
+    g_stamps[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+    g_stamps[4 * wave + 3] = ((unsigned long long)xcc << 32) | nproc;
+  }
+#endif
 }
 
 #ifndef NVL_FAST_U
@@ -591,11 +754,21 @@ __device__ __forceinline__ void run_waves(const G& g, const KArgs& ka) {
 
 template <bool kFast>
 __global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
-  run_waves<kFast, kFast ? NVL_FAST_U : 1>(g, ka);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+#if !defined(NVL_STATIC_ONLY)
+  if constexpr (kFast) {
+    if (g.J == 1) {
+      run_dynamic<NVL_FAST_U>(g, ka, lds);
+      return;
+    }
+  }
+#endif
+  run_waves<kFast, kFast ? NVL_FAST_U : 1>(g, ka, lds);
 }
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
-  run_waves<false, 1>(g, ka);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  run_waves<false, 1>(g, ka, lds);
 }
 
 // Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.
@@ -707,6 +880,12 @@ uint32_t fixed_grid(int num_cu, uint64_t len, uint64_t n) {
 }
 
 uint32_t waves_per_wg() { return dev::kWavesPerWG; }
+
+#if defined(NVL_DIAG_STAMPS)
+extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st) {
   const uint32_t tpb = 256;

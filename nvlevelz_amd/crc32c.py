@@ -140,6 +140,56 @@ def extend_fixed(buf, stride: int, length: int, n: int, init=0, *, mask: bool = 
     return out
 
 
+class FixedBatch:
+    """A validated fixed-stride batch whose launch does no host work beyond the
+    C call: arguments are checked and converted once, the workspace is sized
+    once, and :meth:`launch` re-enqueues the same batch on the same stream
+    (e.g. a table's blocks re-verified, or the bench loop).  The output is
+    ``self.out`` (int32 device tensor holding the u32 bit patterns)."""
+
+    def __init__(self, buf, stride: int, length: int, n: int, init=0, *, mask: bool = False,
+                 base_offset: int = 0, out=None, workspace=None, stream=None):
+        torch = _torch()
+        _require_dev(buf, "buf", (torch.uint8, torch.int8))
+        if n < 0 or length < 0 or stride < 0 or base_offset < 0:
+            raise ValueError("negative size")
+        if n and base_offset + (n - 1) * stride + length > buf.numel():
+            raise ValueError("batch extends past the end of buf")
+        self.buf = buf
+        self.out = out if out is not None else torch.empty(n, dtype=torch.int32, device=buf.device)
+        _require_dev(self.out, "out", (torch.int32, torch.uint32))
+        if self.out.numel() < n:
+            raise ValueError("out too small")
+        self.init = init
+        init_ptr, init_all = None, 0
+        if isinstance(init, int):
+            init_all = init & 0xFFFFFFFF
+        else:
+            _require_dev(init, "init", (torch.int32, torch.uint32))
+            if init.numel() < n:
+                raise ValueError("init too small")
+            init_ptr = init.data_ptr()
+        need = lib.nvl_crc32c_fixed_workspace_bytes(stride, length, n)
+        if workspace is None and need:
+            workspace = torch.empty(need, dtype=torch.uint8, device=buf.device)
+        self.workspace = workspace
+        ws_ptr, ws_bytes = None, 0
+        if workspace is not None:
+            ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+        if stream is None:
+            stream = torch.cuda.current_stream(buf.device)
+        self.stream = stream
+        self._args = (buf.data_ptr() + base_offset, stride, length, n, init_ptr, init_all,
+                      self.out.data_ptr(), FLAG_MASK if mask else 0, ws_ptr, ws_bytes, stream.cuda_stream)
+        self._fn = lib.nvl_crc32c_fixed_dev
+
+    def launch(self):
+        rc = self._fn(*self._args)
+        if rc:
+            check(rc, "nvl_crc32c_fixed_dev")
+        return self.out
+
+
 def extend_batch(buf, offsets, lengths, init=0, *, mask: bool = False, out=None, workspace=None):
     """out[i] = Extend(init_i, buf[offsets[i] : offsets[i] + lengths[i]]).
 
@@ -234,5 +284,5 @@ def to_u32(t) -> np.ndarray:
 
 
 __all__ = ["extend", "value", "mask", "unmask", "kMaskDelta", "init", "gpu_accelerated",
-           "extend_fixed", "extend_batch", "extend_batch_host", "extend_fixed_host",
+           "extend_fixed", "FixedBatch", "extend_batch", "extend_batch_host", "extend_fixed_host",
            "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix", "to_u32", "Crc32cError"]

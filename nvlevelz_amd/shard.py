@@ -1,0 +1,61 @@
+"""Multi-GPU sharding of independent blocks.
+
+Every block's CRC is independent, so a batch shards across the GPUs of a node
+with no data-path exchange: buffer i lives on (and is checksummed by) rank
+i mod G (BASELINE config 5, "round-robin").  The only collective is the
+optional gather of the 4-byte results to one rank, done with
+torch.distributed (RCCL over xGMI on the GPU box, gloo in the CPU tests) in
+ONE all_gather of equal-size slices -- never per block.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def local_count(n_total: int, rank: int, world: int) -> int:
+    """Number of round-robin blocks rank owns out of n_total."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    return (n_total - rank + world - 1) // world if n_total > rank else 0
+
+
+def local_ids(n_total: int, rank: int, world: int) -> np.ndarray:
+    """Global block ids owned by rank: rank, rank+G, rank+2G, ..."""
+    return np.arange(rank, n_total, world, dtype=np.int64)
+
+
+def interleave(parts, n_total: int) -> np.ndarray:
+    """Inverse of the round-robin split: parts[r] holds rank r's CRCs in local order."""
+    world = len(parts)
+    out = np.empty(n_total, dtype=np.uint32)
+    for r, p in enumerate(parts):
+        p = np.asarray(p, dtype=np.uint32)
+        assert p.size == local_count(n_total, r, world)
+        out[r::world] = p
+    return out
+
+
+def gather_crcs(local, n_total: int, group=None):
+    """All-gather every rank's CRC slice (int32 tensor, round-robin order) and
+    return the global u32 array in block order on every rank.
+
+    Slices are padded to a common length so the exchange is one all_gather
+    call (bucketed: 4 bytes per block, e.g. 40 MB for 10^7 blocks)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    per = local_count(n_total, 0, world)  # rank 0 owns the most
+    buf = torch.zeros(per, dtype=torch.int32, device=local.device)
+    buf[:local.numel()] = local
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf, group=group)
+    parts = [o[:local_count(n_total, r, world)].cpu().numpy().view(np.uint32) for r, o in enumerate(outs)]
+    return interleave(parts, n_total)
+
+
+def digest(crcs: np.ndarray) -> int:
+    """crc32c::Value over the little-endian u32 array (SURVEY.md §8d digest),
+    computed with the engine's host path."""
+    from . import crc32c
+    return crc32c.value(np.ascontiguousarray(crcs, dtype="<u4").view(np.uint8))

@@ -1,0 +1,104 @@
+"""The GF(2) identities the HIP engine rests on, and a step-by-step model of
+its decomposition (tests/kernel_model.py), checked against the oracle on the
+CPU.  Catches a wrong butterfly order, end-alignment, masking, ~init
+injection or wave-record fix-up before any GPU run."""
+import random
+
+import numpy as np
+import pytest
+
+import kernel_model as km
+
+
+def test_slice_tables_match_oracle_steps(port):
+    for b in range(256):
+        assert km.T[0][b] == (km.raw_bytes(0, bytes([b])))
+        for k in range(1, 4):
+            assert km.T[k][b] == km.raw_bytes(0, bytes([b]) + bytes(k))
+
+
+def test_shift_is_zero_feed():
+    rng = random.Random(1)
+    for _ in range(50):
+        v = rng.getrandbits(32)
+        n = rng.randrange(0, 300)
+        assert km.shift(v, n) == km.raw_bytes(v, bytes(n))
+
+
+def test_extend_identities(port):
+    rng = random.Random(2)
+    data = bytes(port.fill(77, 0, 20000))
+    for _ in range(100):
+        a = rng.randrange(0, 5000)
+        b = rng.randrange(0, 5000)
+        A, B = data[:a], data[a:a + b]
+        init = rng.getrandbits(32)
+        # Extend(init, D) = ~(shift(~init, |D|) ^ raw(0, D))
+        want = port.extend(init, A)
+        s = (~init) & 0xFFFFFFFF
+        assert (~(km.shift(s, len(A)) ^ km.raw_bytes(0, A))) & 0xFFFFFFFF == want
+        # raw(0, A||B) = shift(raw(0, A), |B|) ^ raw(0, B)
+        assert km.raw_bytes(0, A + B) == km.shift(km.raw_bytes(0, A), len(B)) ^ km.raw_bytes(0, B)
+        # crc(A||B) = shift(crc(A), |B|) ^ crc(B)   (standard combine)
+        assert port.value(A + B) == km.shift(port.value(A), len(B)) ^ port.value(B)
+        if len(A) >= 4:
+            # state injection into the first word: raw(s, w||rest) = raw(0, (w^s)||rest)
+            w = int.from_bytes(A[:4], "little") ^ s
+            assert km.raw_bytes(s, A) == km.raw_bytes(0, w.to_bytes(4, "little") + A[4:])
+        # leading zeros are invisible to a zero-state register
+        assert km.raw_bytes(0, bytes(rng.randrange(0, 70)) + A) == km.raw_bytes(0, A)
+
+
+def test_byte_sliced_operators():
+    rng = random.Random(3)
+    for op, dist in [(km.COMB[k], 64 << k) for k in range(6)] + [(km.SH4096, 4096)]:
+        for _ in range(20):
+            v = rng.getrandbits(32)
+            assert km.apply_op(op, v) == km.shift(v, dist)
+
+
+def test_fast_path_transposed_fold(port):
+    """Fast path: lane 4q+r holds chunk position 16r+q after the quad
+    transpose; the butterfly over lane bits (0,1,2,3,4,5) must use distances
+    (1024, 2048, 64, 128, 256, 512) bytes."""
+    data = bytes(port.fill(5, 0, 4096))
+    # the transpose itself: lane l's load j holds bytes [1024j+16l, +16)
+    M = [[(l, j) for j in range(4)] for l in range(64)]
+
+    def stage(M, m, bit):
+        return [[M[l ^ m][j ^ m] if ((j >> bit) & 1) != (((l & 3) >> bit) & 1) else M[l][j]
+                 for j in range(4)] for l in range(64)]
+    M = stage(stage(M, 2, 1), 1, 0)
+    lanes = []
+    for l in range(64):
+        piece = b"".join(data[1024 * j + 16 * src:1024 * j + 16 * src + 16] for (src, j) in M[l])
+        q, r = l >> 2, l & 3
+        assert piece == data[64 * (16 * r + q):64 * (16 * r + q) + 64]
+        lanes.append(km.raw_bytes(0, piece))
+    ops = [km.COMB[i] for i in (4, 5, 0, 1, 2, 3)]
+    g = lanes
+    for lev in range(6):
+        pt = [g[l ^ (1 << lev)] for l in range(64)]
+        g = [km.apply_op(ops[lev], pt[l] if (l >> lev) & 1 else g[l]) ^ (g[l] if (l >> lev) & 1 else pt[l])
+             for l in range(64)]
+    assert len(set(g)) == 1 and g[0] == km.raw_bytes(0, data)
+    assert (~km.raw_bytes(0xFFFFFFFF, data)) & 0xFFFFFFFF == port.value(data)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_general_path_model(port, seed):
+    """End-aligned chunks, masking, injection, per-wave ranges, records and
+    fix-up, with more waves than chunks and buffers straddling waves."""
+    rng = random.Random(seed)
+    mem = bytes(port.fill(1000 + seed, 0, 120000))
+    bufs, pos = [], 64
+    for _ in range(rng.randrange(1, 7)):
+        L = rng.choice([0, 1, 2, 3, 4, 5, 17, 63, 64, 65, 4095, 4096, 4097, 8192, 9000, 13000, 20000])
+        pos += rng.randrange(0, 40)
+        bufs.append((pos, L))
+        pos += L
+    inits = [rng.getrandbits(32) for _ in bufs]
+    nw = rng.choice([1, 2, 3, 5, 16, 33])
+    got = km.batch(mem, bufs, inits, nw)
+    want = [port.extend(i, mem[a:a + L]) for (a, L), i in zip(bufs, inits)]
+    assert got == want

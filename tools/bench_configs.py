@@ -1,0 +1,63 @@
+"""Time BASELINE configs 2-4 through the C ABI (HIP events, median of R reps).
+    python tools/bench_configs.py [--lib build/libnvl_crc32c_X.so] [--configs 2,3,4]"""
+import argparse, ctypes, json, os, sys
+import numpy as np, torch
+ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from nvlevelz_amd import _lib
+import oracle
+ap = argparse.ArgumentParser(); ap.add_argument("--lib"); ap.add_argument("--configs", default="2,3,4")
+ap.add_argument("--reps", type=int, default=20)
+a = ap.parse_args()
+lib = _lib.lib
+if a.lib:
+    lib = ctypes.CDLL(os.path.abspath(a.lib), mode=os.RTLD_LOCAL)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        f = getattr(lib, name); f.restype = res; f.argtypes = args
+dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
+assert lib.nvl_crc32c_init(0) == 0
+st = torch.cuda.current_stream().cuda_stream
+g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
+p = oracle.port()
+
+def timeit(fn, reps):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    for j in range(reps):
+        ev[2*j].record(); fn(); ev[2*j+1].record()
+    torch.cuda.synchronize()
+    return float(np.median([ev[2*j].elapsed_time(ev[2*j+1]) for j in range(reps)])) * 1e-3
+
+for c in a.configs.split(","):
+    c = int(c)
+    if c in (2, 4):
+        cfg = g[f"cfg{c}"]; n, L = cfg["n"], cfg["len"]
+        buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
+        lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, cfg["seed"], None)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        wsb = max(1, lib.nvl_crc32c_fixed_workspace_bytes(L, L, n))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fn = lambda: lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(), wsb, st)
+        alg = n * (L + 4)
+    else:
+        cfg = g["cfg3"]; total = cfg["total"]
+        lens = p.cfg3_lengths(cfg["len_seed"], total)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        n = lens.size
+        buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+        lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, cfg["seed"], None)
+        o = torch.from_numpy(offs).to(dev); m = torch.from_numpy(lens.astype(np.int64)).to(dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        wsb = lib.nvl_crc32c_batch_workspace_bytes(n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fn = lambda: lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0, ws.data_ptr(), wsb, st)
+        alg = total + 12 * n
+    t = timeit(fn, a.reps if c != 4 else max(3, a.reps // 4))
+    res = out.cpu().numpy().view(np.uint32)
+    ok = p.digest(res) == cfg["digest"]
+    print(json.dumps({"config": c, "n": int(n), "bytes": int(alg), "median_us": round(t * 1e6, 1),
+                      "GB/s": round(alg / t / 1e9, 1), "GiB/s": round((alg) / t / 2**30, 1),
+                      "frac_of_8TBs": round(alg / t / 8e12, 4), "digest_ok": ok}))
+    del buf
+    torch.cuda.empty_cache()

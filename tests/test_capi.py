@@ -111,3 +111,37 @@ def test_product_does_not_import_oracle():
                 text = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in text and "oracle_crc32c" not in text, f
                 assert "liboracle" not in text and "_ref/" not in text, f
+
+
+def test_leveldb_mirror_header(tmp_path):
+    """include/nvl_crc32c_leveldb.h: util/crc32c.h's API compiled and run in C++
+    against util/crc32c_test.cc's known answers (CPU path, no GPU needed)."""
+    src = tmp_path / "t.cc"
+    src.write_text(r'''
+#include <string.h>
+#include <stdio.h>
+#include "nvl_crc32c_leveldb.h"
+using namespace leveldb::crc32c;
+int main() {
+  char buf[32];
+  memset(buf, 0, 32); if (Value(buf, 32) != 0x8a9136aa) return 1;
+  memset(buf, 0xff, 32); if (Value(buf, 32) != 0x62a8ab43) return 2;
+  for (int i = 0; i < 32; i++) buf[i] = i;
+  if (Value(buf, 32) != 0x46dd794e) return 3;
+  for (int i = 0; i < 32; i++) buf[i] = 31 - i;
+  if (Value(buf, 32) != 0x113fdb5c) return 4;
+  if (Value("a", 1) == Value("foo", 3)) return 5;
+  if (Value("hello world", 11) != Extend(Value("hello ", 6), "world", 5)) return 6;
+  uint32_t crc = Value("foo", 3);
+  if (crc == Mask(crc) || crc == Mask(Mask(crc))) return 7;
+  if (crc != Unmask(Mask(crc)) || crc != Unmask(Unmask(Mask(Mask(crc))))) return 8;
+  if (Value("TestCRCBuffer", 13) != 0xdcbc59fa) return 9;
+  return 0;
+}
+''')
+    inc = os.path.join(ROOT, "include")
+    lib = os.path.join(ROOT, "nvlevelz_amd")
+    exe = tmp_path / "t"
+    subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", inc, str(src), "-L", lib, "-lnvl_crc32c",
+                    f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+    subprocess.run([str(exe)], check=True)

@@ -103,21 +103,21 @@ DeviceState* current_state(int* rc) {
   return state_for(dev, rc);
 }
 
-size_t batch_ws_layout(uint64_t n, int num_cu, size_t* off_cs, size_t* off_recs, size_t* off_tmp) {
+// Variable-batch workspace: [counts n+1][chunk_start n+1][unit map][records][scan scratch]
+size_t batch_ws_layout(uint64_t n, int num_cu, size_t* off_cs, size_t* off_map, size_t* off_recs, size_t* off_tmp) {
   const size_t cnt = align_up((n + 1) * sizeof(uint64_t), 256);
   const size_t cs = cnt;
-  const size_t recs = align_up(2ull * (size_t)num_cu * waves_per_wg() * sizeof(Rec), 256);
+  const size_t map = align_up(var_unit_map_bytes(num_cu), 256);
+  const size_t recs = align_up(var_recs_bytes(num_cu), 256);
   const size_t tmp = align_up(scan_temp_bytes(n + 1), 256);
   *off_cs = cnt;
-  *off_recs = cnt + cs;
-  *off_tmp = cnt + cs + recs;
-  return cnt + cs + recs + tmp;
+  *off_map = cnt + cs;
+  *off_recs = cnt + cs + map;
+  *off_tmp = cnt + cs + map + recs;
+  return cnt + cs + map + recs + tmp;
 }
 
-size_t fixed_ws_bytes(uint64_t len, uint64_t n, int num_cu) {
-  if (len <= 4096 || n == 0) return 0;
-  return 2ull * fixed_grid(num_cu, len, n) * waves_per_wg() * sizeof(Rec);
-}
+size_t fixed_ws_bytes(uint64_t len, uint64_t n, int num_cu) { return fixed_recs_bytes(num_cu, len, n); }
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? NVL_CRC32C_OK : NVL_CRC32C_EHIP; }
 
@@ -147,8 +147,8 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out) return NVL_CRC32C_EINVAL;
   if (n >= (1ull << 31) - 2) return NVL_CRC32C_EINVAL;
-  size_t off_cs, off_recs, off_tmp;
-  const size_t need = batch_ws_layout(n, s->num_cu, &off_cs, &off_recs, &off_tmp);
+  size_t off_cs, off_map, off_recs, off_tmp;
+  const size_t need = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_tmp);
   bool own = false;
   if (!ws) {
     if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
@@ -159,14 +159,15 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint64_t* cnt = reinterpret_cast<uint64_t*>(w);
   uint64_t* cs = reinterpret_cast<uint64_t*>(w + off_cs);
+  uint64_t* unit_first = reinterpret_cast<uint64_t*>(w + off_map);
   Rec* recs = reinterpret_cast<Rec*>(w + off_recs);
   void* tmp = w + off_tmp;
   hipError_t e = launch_var_counts(lengths, n, cnt, st);
   if (e == hipSuccess) e = exclusive_scan_u64(tmp, need - off_tmp, cnt, cs, n + 1, st);
   if (e == hipSuccess) {
     LaunchCtx lc{st, s->num_cu, s->tables};
-    e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, n, init, init_all, out, flags,
-                   recs);
+    e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, unit_first, n, init, init_all, out,
+                   flags, recs);
   }
   if (own) (void)hipFreeAsync(ws, st);
   return hip_rc(e);
@@ -328,8 +329,8 @@ size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, uint64_t 
 size_t nvl_crc32c_batch_workspace_bytes(uint64_t n) {
   int rc = NVL_CRC32C_OK;
   DeviceState* s = current_state(&rc);
-  size_t a, b, c;
-  return batch_ws_layout(n, s ? s->num_cu : 256, &a, &b, &c);
+  size_t a, b, c, d;
+  return batch_ws_layout(n, s ? s->num_cu : 256, &a, &b, &c, &d);
 }
 
 int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
@@ -383,8 +384,8 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   hipStream_t st;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
-  size_t off_cs, off_recs, off_tmp;
-  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_recs, &off_tmp);
+  size_t off_cs, off_map, off_recs, off_tmp;
+  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_tmp);
   const size_t dbytes = total + n * 4 + ws + 512;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) {
     (void)hipStreamDestroy(st);

@@ -17,7 +17,7 @@ namespace nvl {
 //   [8192,  8256)  x2n[64]            x^(2^k) mod P
 constexpr uint32_t kTableWords = 8256;
 
-// A portion of one buffer processed by one wave (fix-up input).
+// A portion of one buffer processed inside one work unit (fix-up input).
 struct Rec {
   unsigned long long buf;  // buffer index, kNoBuf when unused
   uint32_t raw;            // raw register of the portion (ends at the portion end)
@@ -36,13 +36,14 @@ void build_device_tables(uint32_t* words /* kTableWords */);
 
 hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
                         const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs);
-uint32_t fixed_grid(int num_cu, uint64_t len, uint64_t n);
-uint32_t waves_per_wg();
+size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n);  // workspace of launch_fixed
+size_t var_recs_bytes(int num_cu);                               // record part of launch_var's workspace
+size_t var_unit_map_bytes(int num_cu);                           // unit map part of launch_var's workspace
 
 hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st);
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
-                      const uint64_t* chunk_start, uint64_t n, const uint32_t* init, uint32_t init_all,
-                      uint32_t* out, uint32_t flags, Rec* recs);
+                      const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs);
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

@@ -253,6 +253,9 @@ struct FixedGeom {
     const uint32_t ini = init ? init[i] : init_all;
     return BufInfo{base + i * stride, len, J, ~ini};
   }
+  __device__ __forceinline__ void locate_unit(uint32_t, uint64_t t, uint64_t& i, uint32_t& c) const {
+    locate(t, i, c);
+  }
 };
 
 struct VarGeom {
@@ -260,6 +263,7 @@ struct VarGeom {
   const uint64_t* offsets;
   const uint64_t* lengths;
   const uint64_t* chunk_start;  // n+1 entries, exclusive prefix of J_i
+  const uint64_t* unit_first;   // per work unit: the buffer holding its first chunk
   uint64_t n;
   const uint32_t* init;
   uint32_t init_all;
@@ -273,6 +277,11 @@ struct VarGeom {
     i = lo;
     c = (uint32_t)(t - chunk_start[lo]);
   }
+  // Start of work unit u (chunk t = its first): one load instead of a search.
+  __device__ __forceinline__ void locate_unit(uint32_t u, uint64_t t, uint64_t& i, uint32_t& c) const {
+    i = unit_first[u];
+    c = (uint32_t)(t - chunk_start[i]);
+  }
   __device__ __forceinline__ BufInfo info(uint64_t i) const {
     const uint64_t L = lengths[i];
     const uint32_t J = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
@@ -281,106 +290,173 @@ struct VarGeom {
   }
 };
 
-// Loaded bytes of one lane's piece (20 dwords covers a misaligned piece).
-struct Piece {
+// Load modes: kAligned = 16-B aligned buffer whose length is a multiple of 4096
+// (every chunk full, no masking: configs 2, 4, 5); kGeneral = any alignment and
+// length (partial head chunk, realignment, predicated loads: config 3).
+enum LoadMode : int { kAligned = 0, kGeneral = 1 };
+
+// Registers of one chunk as loaded: row j (j = 0..3) is the coalesced 1 KiB
+// wave load of chunk bytes [1024j, 1024j+1024), lane l holding 16 B at 16l; in
+// kGeneral the rows are loaded from the 16-B aligned address below the chunk
+// start and d[16..19] holds the aligned vector just past row 3.
+struct Chunk {
   uint32_t d[20];
 };
 
-// 4x4 transpose of 16-byte slots inside each lane quad (DPP quad_perm):
-// afterwards lane 4q+r holds, in slot s, what lane 4q+s held in slot r.
-__device__ __forceinline__ void quad_transpose(int lane, uint32_t (&d)[20]) {
-  const int r = lane & 3;
-  uint32_t t[16];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {  // stage 1: swap 2x2 blocks across lane bit 1
-    const bool take = ((j >> 1) & 1) != ((r >> 1) & 1);
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const uint32_t o = dpp_xor2(d[4 * (j ^ 2) + x]);
-      t[4 * j + x] = take ? o : d[4 * j + x];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {  // stage 2: swap within 2x2 blocks across lane bit 0
-    const bool take = (j & 1) != (r & 1);
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const uint32_t o = dpp_xor1(t[4 * (j ^ 1) + x]);
-      d[4 * j + x] = take ? o : t[4 * j + x];
-    }
-  }
+__device__ __forceinline__ uintptr_t chunk_end(const BufInfo& bi, uint32_t c) {
+  return (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
 }
 
-// Fast path (16-B aligned, full 4 KiB chunks): four fully coalesced 1 KiB
-// loads (row j = bytes [1024j, 1024j+1024) of the chunk, lane l at 16l).  After
-// quad_transpose (in build_words) lane 4q+r holds the contiguous 64-byte piece
-// at chunk position P = 16r + q.
-template <bool kFast>
-__device__ __forceinline__ void load_piece(const BufInfo& bi, uint32_t c, int lane, Piece& pc) {
-  const uintptr_t ce = (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
-  const uintptr_t ps = ce - (uintptr_t)(64 * (64 - lane));
-  if constexpr (kFast) {
+template <int M>
+__device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int lane, Chunk& ch) {
+  const uintptr_t ce = chunk_end(bi, c);
+  if constexpr (M == kAligned) {
 #if defined(NVL_ABL_NOLOAD)  // ablation: synthetic data, no global loads
 #pragma unroll
-    for (int k = 0; k < 16; ++k) pc.d[k] = (uint32_t)(ps >> 4) * 2654435761u + (uint32_t)k * 40503u;
+    for (int k = 0; k < 16; ++k) ch.d[k] = (uint32_t)(ce >> 4) * 2654435761u + (uint32_t)(k * 40503 + lane);
     return;
 #endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-#if defined(NVL_ABL_STRIDED)  // ablation: the v1 lane-contiguous (64-B stride) loads
-      const u32x4 v = ld16(ps + 16u * (uint32_t)j);
-#else
       const u32x4 v = ld16(ce - kChunk + 1024u * (uint32_t)j + 16u * (uint32_t)lane);
-#endif
-      pc.d[4 * j + 0] = v.x; pc.d[4 * j + 1] = v.y; pc.d[4 * j + 2] = v.z; pc.d[4 * j + 3] = v.w;
+      ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
     }
   } else {
     if (bi.len < 4) return;  // tiny path reads its own bytes
-    const uint32_t m = (uint32_t)(ce & 15u);
-    const uintptr_t a = ps - m;
     const uintptr_t p = (uintptr_t)bi.p;
+    if (ce - kChunk < p + 4) {
+      // Head chunk: 16-B aligned loads below the chunk start (never crossing
+      // into a page the buffer does not touch), vectors wholly before the
+      // buffer skipped; the aligned vector just past row 3 is the same for
+      // every lane: a scalar load (SGPRs) ending inside ce's 16-B granule.
+      const uint32_t m = (uint32_t)(ce & 15u);
+      const uintptr_t A = ce - kChunk - m;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const bool ok = (j < 4 || m != 0) && (a + 16u * (uint32_t)j + 16u > p);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (ok) v = ld16(a + 16u * (uint32_t)j);
-      pc.d[4 * j + 0] = v.x; pc.d[4 * j + 1] = v.y; pc.d[4 * j + 2] = v.z; pc.d[4 * j + 3] = v.w;
+      for (int j = 0; j < 4; ++j) {
+        const uintptr_t addr = A + 1024u * (uint32_t)j + 16u * (uint32_t)lane;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (addr + 16u > p) v = ld16(addr);
+        ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+      }
+      u32x4 x = {0u, 0u, 0u, 0u};
+      if (m != 0) x = *reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(A + kChunk);
+      ch.d[16] = x.x; ch.d[17] = x.y; ch.d[18] = x.z; ch.d[19] = x.w;
+    } else {
+      // Body chunk: every byte of [ce-4096-3, ce) lies inside the buffer, so
+      // the rows are loaded at the DWORD-aligned address below the chunk
+      // start (gfx950 serves 4-B aligned dwordx4 at full rate, byte-misaligned
+      // at ~80 %: tools/diag/unaligned.hip); the dword past row 3 (scalar)
+      // completes lane 63.
+      const uint32_t r = (uint32_t)(ce & 3u);
+      const uintptr_t A4 = ce - kChunk - r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + 16u * (uint32_t)lane);
+        ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+      }
+      ch.d[16] = r ? *reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(A4 + kChunk) : 0u;
+      ch.d[17] = ch.d[18] = ch.d[19] = 0u;
     }
   }
 }
 
-template <int Q0>
-__device__ __forceinline__ void realign(const Piece& pc, uint32_t r, uint32_t (&w)[16]) {
+// 4x4 transpose of 16-byte slots inside each lane quad (DPP quad_perm):
+// afterwards lane 4q+r holds, in slot s, what lane 4q+s held in slot r.
+__device__ __forceinline__ void quad_transpose(int lane, uint32_t (&d)[16]) {
+  const int r = lane & 3;
+  const bool t1[4] = {(r >> 1) != 0, (r >> 1) != 0, (r >> 1) == 0, (r >> 1) == 0};  // bit1(j) != bit1(r)
+  const bool t0[4] = {(r & 1) != 0, (r & 1) == 0, (r & 1) != 0, (r & 1) == 0};      // bit0(j) != bit0(r)
 #pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(pc.d[Q0 + k + 1], pc.d[Q0 + k], r);
+  for (int x = 0; x < 4; ++x) {  // one dword column at a time: 4 live temporaries
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = d[4 * j + x];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // stage 1: swap 2x2 blocks across lane bit 1
+      const uint32_t o = dpp_xor2(a[j ^ 2]);
+      b[j] = t1[j] ? o : a[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // stage 2: swap within 2x2 blocks across lane bit 0
+      const uint32_t o = dpp_xor1(b[j ^ 1]);
+      d[4 * j + x] = t0[j] ? o : b[j];
+    }
+  }
 }
 
-// The 16 little-endian words of this lane's piece, realigned, with the head
-// masking and ~init injection applied (wave-uniform control flow).
-template <bool kFast>
-__device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int lane, const Piece& pc,
+// The lane's 16 words, transposed so lane 4q+r holds chunk piece P = 16r + q
+// (64 contiguous bytes), with the ~init injection and, on the head chunk, the
+// zero-masking of bytes before the buffer start.
+template <int M>
+__device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int lane, const Chunk& ch,
                                             uint32_t (&w)[16]) {
-  if constexpr (kFast) {
-    Piece t = pc;
-#if !defined(NVL_ABL_STRIDED) && !defined(NVL_ABL_NOLOAD)
-    quad_transpose(lane, t.d);
-#endif
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k] = t.d[k];
-    if (c == 0 && lane == 0) w[0] ^= bi.s;  // position 0 is lane 0 in both layouts
+  for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
+  if constexpr (M == kAligned) {
+#if !defined(NVL_ABL_NOLOAD)
+    quad_transpose(lane, w);
+#endif
+    if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0
   } else {
-    const uintptr_t ce = (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
-    const uint32_t m = (uint32_t)(ce & 15u);
-    const uint32_t r = m & 3u;
-    switch (m >> 2) {
-      case 0: realign<0>(pc, r, w); break;
-      case 1: realign<1>(pc, r, w); break;
-      case 2: realign<2>(pc, r, w); break;
-      default: realign<3>(pc, r, w); break;
+    const uintptr_t ce = chunk_end(bi, c);
+    const bool head = ce - kChunk < (uintptr_t)bi.p + 4;
+    // Shift the loaded rows left by sh bytes: head chunks were loaded from the
+    // 16-B aligned address below the chunk start (sh = ce & 15), body chunks
+    // from the 4-B aligned one (sh = ce & 3).  Lane l's bytes continue in lane
+    // l+1 (DPP wave_shl:1); lane 63 continues in lane 0 of the next row
+    // (wave_rol:1) or, after row 3, in the scalar extra.
+    const uint32_t sh = head ? (uint32_t)(ce & 15u) : (uint32_t)(ce & 3u);
+#if defined(NVL_ABL_NOREALIGN)
+    if (false) {
+#else
+    if (sh != 0) {
+#endif
+      const uint32_t r = sh & 3u;
+      if (sh >= 4) {  // head chunk with a dword shift: all four next-lane dwords
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t e[8];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const uint32_t old = j < 3 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)ch.d[4 * (j + 1) + x], 0x134, 0xF, 0xF, true)
+                                       : ch.d[16 + x];
+            e[x] = ch.d[4 * j + x];
+            e[4 + x] = (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)ch.d[4 * j + x], 0x130, 0xF, 0xF, false);
+          }
+          // dword shift sh>>2 as two levels of v_perm_b32 whose selector picks
+          // a whole source dword (a plain select here becomes a scratch-indexed
+          // load), then v_alignbyte_b32 for the byte shift sh&3.
+          const uint32_t s1 = (sh & 8u) ? 0x07060504u : 0x03020100u;
+          const uint32_t s0 = (sh & 4u) ? 0x07060504u : 0x03020100u;
+          uint32_t f[6], gg[5];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) f[k] = __builtin_amdgcn_perm(e[k + 2], e[k], s1);
+#pragma unroll
+          for (int k = 0; k < 5; ++k) gg[k] = __builtin_amdgcn_perm(f[k + 1], f[k], s0);
+#pragma unroll
+          for (int x = 0; x < 4; ++x) w[4 * j + x] = __builtin_amdgcn_alignbyte(gg[x + 1], gg[x], r);
+        }
+      } else {  // byte shift only: one next-lane dword per row
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t old = j < 3 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)ch.d[4 * (j + 1)], 0x134, 0xF, 0xF, true)
+                                     : ch.d[16];
+          const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)ch.d[4 * j], 0x130, 0xF, 0xF, false);
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+            w[4 * j + x] = __builtin_amdgcn_alignbyte(x < 3 ? ch.d[4 * j + x + 1] : nx, ch.d[4 * j + x], r);
+        }
+      }
     }
+    quad_transpose(lane, w);
     const uintptr_t p = (uintptr_t)bi.p;
-    if (ce - kChunk < p + 4) {  // chunk holds the buffer head (or the tail of its ~init)
-      const uintptr_t ps = ce - (uintptr_t)(64 * (64 - lane));
+#if defined(NVL_ABL_NOMASK)
+    if (false) {
+#else
+    if (head) {  // chunk holds the buffer head (or the tail of its ~init)
+#endif
+      const uint32_t P = 16u * (uint32_t)(lane & 3) + (uint32_t)(lane >> 2);
+      const uintptr_t ps = ce - kChunk + 64u * P;
       int64_t rel = (int64_t)(p - ps);  // bytes of this piece before the buffer
       rel = rel < -8 ? -8 : (rel > 72 ? 72 : rel);
       const uint32_t s = bi.s;
@@ -399,15 +475,14 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
 
 // Raw (zero-state, ~init injected) registers of U chunks, wave-uniform.  The
 // U serial slice-by-4 chains and U butterflies are interleaved so each wave
-// keeps U independent LDS round trips in flight (the kernel is bound by the
-// chain's LDS latency, not by LDS bandwidth).
-template <bool kFast, int U>
+// keeps U independent LDS round trips in flight.
+template <int M, int U>
 __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo (&bi)[U],
-                                          const uint32_t (&c)[U], int lane, const Piece (&pc)[U],
+                                          const uint32_t (&c)[U], int lane, const Chunk (&ch)[U],
                                           uint32_t (&raw)[U]) {
   uint32_t w[U][16];
 #pragma unroll
-  for (int u = 0; u < U; ++u) build_words<kFast>(bi[u], c[u], lane, pc[u], w[u]);
+  for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u]);
   uint32_t crc[U];
 #if defined(NVL_ABL_NOCOMPUTE)  // ablation: keep the loads live, skip every lookup
 #pragma unroll
@@ -419,44 +494,61 @@ __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb
   }
   return;
 #endif
-  {
 #pragma unroll
-    for (int u = 0; u < U; ++u) crc[u] = w[u][0];
+  for (int u = 0; u < U; ++u) crc[u] = w[u][0];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+  for (int k = 0; k < 16; ++k) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
-    }
+    for (int u = 0; u < U; ++u) crc[u] = slice4(lds, crc[u], lb) ^ (k < 15 ? w[u][k + 1] : 0u);
   }
-
-  // Lane -> stream position: general path P = lane; fast path (transposed
-  // rows) P = 16*(lane&3) + (lane>>2), so lane bits 0,1 step 1024/2048 bytes
-  // and bits 2..5 step 64..512 bytes.
-  constexpr bool kT = kFast && !NVL_ABL_LAYOUT_STRIDED;
+  // Lane -> stream position P = 16*(lane&3) + (lane>>2): lane bits 0,1 step
+  // 1024/2048 bytes (comb tables 4, 5), bits 2..5 step 64..512 (tables 0..3).
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, kT ? 4 : 0>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, 4>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, kT ? 5 : 1>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, 5>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, kT ? 0 : 2>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, 0>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, kT ? 1 : 3>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, 1>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, kT ? 2 : 4>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, 2>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, kT ? 3 : 5>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, 3>(lds, crc[u], lane);
 #pragma unroll
   for (int u = 0; u < U; ++u) raw[u] = crc[u];
 }
 
-template <bool kFast>
+// Chain + butterfly of one chunk from its built words.
+__device__ __forceinline__ uint32_t chain_fold(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[16],
+                                               int lane) {
+#if defined(NVL_ABL_NOCOMPUTE)
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) x ^= w[k];
+  return x ^ lane_xor<5>(x);
+#else
+  uint32_t crc = w[0];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) crc = slice4(lds, crc, lb) ^ (k < 15 ? w[k + 1] : 0u);
+  crc = fold_level<0, 4>(lds, crc, lane);
+  crc = fold_level<1, 5>(lds, crc, lane);
+  crc = fold_level<2, 0>(lds, crc, lane);
+  crc = fold_level<3, 1>(lds, crc, lane);
+  crc = fold_level<4, 2>(lds, crc, lane);
+  crc = fold_level<5, 3>(lds, crc, lane);
+  return crc;
+#endif
+}
+
+template <int M>
 __device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo& bi,
-                                              uint32_t c, int lane, const Piece& pc) {
+                                              uint32_t c, int lane, const Chunk& ch) {
   const BufInfo b1[1] = {bi};
   const uint32_t c1[1] = {c};
-  const Piece p1[1] = {pc};
+  const Chunk h1[1] = {ch};
   uint32_t r1[1];
-  group_raw<kFast, 1>(lds, lb, b1, c1, lane, p1, r1);
+  group_raw<M, 1>(lds, lb, b1, c1, lane, h1, r1);
   return r1[0];
 }
 
@@ -473,16 +565,24 @@ __device__ __forceinline__ uint32_t tiny_crc(const uint8_t* lds, const BufInfo& 
 struct KArgs {
   uint32_t* out;
   uint32_t flags;
-  Rec* recs;  // 2 per wave: [2w] = head portion, [2w+1] = tail portion (or nullptr)
+  Rec* recs;  // 2 per work unit: [2u] = head portion, [2u+1] = tail portion (or nullptr)
   const uint32_t* tables;
 };
 
-// Position of one chunk inside a wave's range.
+// Position of one chunk.
 struct Pos {
   uint64_t i;  // buffer
   uint32_t c;  // chunk within the buffer
   BufInfo bi;
 };
+
+template <class G>
+__device__ __forceinline__ Pos unit_start_pos(const G& g, uint32_t u, uint64_t t) {
+  Pos p;
+  g.locate_unit(u, t, p.i, p.c);
+  p.bi = g.info(p.i);
+  return p;
+}
 
 template <class G>
 __device__ __forceinline__ Pos next_pos(const G& g, const Pos& p) {
@@ -497,14 +597,14 @@ __device__ __forceinline__ Pos next_pos(const G& g, const Pos& p) {
   return q;
 }
 
-// Per-wave accumulation over consecutive chunks (wave-uniform).
-struct WaveState {
+// Accumulation over the consecutive chunks of one work unit (wave-uniform).
+struct UnitState {
   uint32_t acc, cnt;
   bool from_zero;
   Rec head;
 };
 
-__device__ __forceinline__ void consume(WaveState& st, const Pos& p, uint32_t raw, const uint8_t* lds, int lane,
+__device__ __forceinline__ void consume(UnitState& st, const Pos& p, uint32_t raw, const uint8_t* lds, int lane,
                                         const KArgs& ka) {
   st.acc = st.cnt ? (shift4096(lds, st.acc, lane) ^ raw) : raw;
   ++st.cnt;
@@ -519,151 +619,55 @@ __device__ __forceinline__ void consume(WaveState& st, const Pos& p, uint32_t ra
   }
 }
 
-#if defined(NVL_DIAG_STAMPS)
-// Diagnostic build only: per-wave {start, after-fill, end} s_memtime stamps
-// and the XCC id, read back with nvl_diag_stamps().
-__device__ unsigned long long g_stamps[4 * 65536];
-#endif
-
-template <bool kFast, int U, class G>
-__device__ __forceinline__ void run_waves(const G& g, const KArgs& ka, uint8_t* lds) {
-#if defined(NVL_DIAG_STAMPS)
-  const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-#endif
-
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerWG + (threadIdx.x >> 6));
-  const uint32_t nw = gridDim.x * kWavesPerWG;
-
-  const uint64_t T = g.total();
-  const uint64_t t0 = T * wave / nw;
-  const uint64_t t1 = T * (wave + 1) / nw;
-
-  // Issue the first chunks' HBM loads before building the LDS tables so the
-  // table fill hides under their latency.
-  Pos p;
-  Pos gp[U];
-  Piece cur[U];
-  const bool grouped = (U > 1) && (t0 + U <= t1);
-  if (t0 < t1) {
-    g.locate(t0, p.i, p.c);
-    p.bi = g.info(p.i);
-    if (grouped) {
-      gp[0] = p;
-#pragma unroll
-      for (int u = 1; u < U; ++u) gp[u] = next_pos(g, gp[u - 1]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) load_piece<kFast>(gp[u].bi, gp[u].c, lane, cur[u]);
-    } else {
-      load_piece<kFast>(p.bi, p.c, lane, cur[0]);
-    }
-  }
-  fill_lds(lds, ka.tables);
-  __syncthreads();
-  const LaneBase lb = make_lane_base(lane);
-#if defined(NVL_DIAG_STAMPS)
-  const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
-#endif
-
-  Rec tail{kNoBuf, 0u, 0u};
-  WaveState st{0u, 0u, true, Rec{kNoBuf, 0u, 0u}};
-  if (t0 < t1) {
-    st.from_zero = (p.c == 0);
-    uint64_t t = t0;
-    // ---- U chunks per step, next U prefetched while these compute ----
-    if constexpr (U > 1) {
-      if (grouped) {
-        while (true) {
-          const bool more = t + 2 * U <= t1;
-          Pos np[U];
-          Piece nxt[U];
-          if (more) {
-            np[0] = next_pos(g, gp[U - 1]);
-#pragma unroll
-            for (int u = 1; u < U; ++u) np[u] = next_pos(g, np[u - 1]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) load_piece<kFast>(np[u].bi, np[u].c, lane, nxt[u]);
-          }
-          BufInfo bis[U];
-          uint32_t cs[U], raws[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            bis[u] = gp[u].bi;
-            cs[u] = gp[u].c;
-          }
-          group_raw<kFast, U>(lds, lb, bis, cs, lane, cur, raws);
-#pragma unroll
-          for (int u = 0; u < U; ++u) consume(st, gp[u], raws[u], lds, lane, ka);
-          t += U;
-          if (!more) break;
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            gp[u] = np[u];
-            cur[u] = nxt[u];
-          }
-        }
-        p = (t < t1) ? next_pos(g, gp[U - 1]) : gp[U - 1];  // chunk t, or the last one consumed
-        if (t < t1) load_piece<kFast>(p.bi, p.c, lane, cur[0]);
-      }
-    }
-    // ---- remaining chunks one at a time (cur[0] holds chunk t) ----
-    for (; t < t1; ++t) {
-      Pos q = p;
-      Piece nxt;
-      if (t + 1 < t1) {
-        q = next_pos(g, p);
-        load_piece<kFast>(q.bi, q.c, lane, nxt);
-      }
-      if (!kFast && p.bi.len < 4) {
-        const uint32_t v = tiny_crc(lds, p.bi);
-        if (lane == 0) ka.out[p.i] = finish(v, ka.flags);
-        st.cnt = 0;
-        st.from_zero = true;
-      } else {
-        consume(st, p, chunk_raw<kFast>(lds, lb, p.bi, p.c, lane, cur[0]), lds, lane, ka);
-      }
-      if (t + 1 < t1) {
-        p = q;
-        cur[0] = nxt;
-      }
-    }
-    if (st.cnt) {
-      if (st.from_zero) tail = Rec{p.i, st.acc, st.cnt};
-      else st.head = Rec{p.i, st.acc, st.cnt};
-    }
-  }
-  if (ka.recs && lane == 0) {
-    ka.recs[2 * wave] = st.head;
-    ka.recs[2 * wave + 1] = tail;
-  }
-#if defined(NVL_DIAG_STAMPS)
-  if (lane == 0 && wave < 65536) {
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_stamps[4 * wave + 0] = ts0;
-    g_stamps[4 * wave + 1] = ts1;
-    g_stamps[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
-    g_stamps[4 * wave + 3] = ((unsigned long long)xcc << 32) | (t1 - t0);
-  }
-#endif
+__device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane) {
+  uint32_t v = 0;
+  if (lane == 0)
+    v = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + kCtrOff), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(v);
 }
 
-// Fixed stride with J == 1 (every chunk is a whole buffer; config 2): the
-// workgroup owns a contiguous range of buffers and its 16 waves pull units of
-// U buffers from an LDS counter, so fast and slow waves of a CU finish
-// together (a static per-wave split left the last wave ~20% behind the mean).
-template <int U>
-__device__ __forceinline__ void run_dynamic(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
 #if defined(NVL_DIAG_STAMPS)
-  const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t nproc = 0;
+// Diagnostic build only: per-wave {start, after-fill, end} s_memrealtime
+// stamps and {XCC id, units}, read back with nvl_diag_stamps().
+__device__ unsigned long long g_stamps[4 * 65536];
+#define NVL_STAMP0() const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime(); uint32_t nproc = 0
+#define NVL_STAMP1() const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime()
+#define NVL_COUNT() (++nproc)
+#define NVL_STAMP_END()                                                                     \
+  do {                                                                                      \
+    const uint32_t wave_ = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);                   \
+    if ((threadIdx.x & 63) == 0 && wave_ < 65536) {                                         \
+      unsigned xcc_;                                                                        \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
+      g_stamps[4 * wave_ + 0] = ts0;                                                        \
+      g_stamps[4 * wave_ + 1] = ts1;                                                        \
+      g_stamps[4 * wave_ + 2] = __builtin_amdgcn_s_memrealtime();                           \
+      g_stamps[4 * wave_ + 3] = ((unsigned long long)xcc_ << 32) | nproc;                   \
+    }                                                                                       \
+  } while (0)
+#else
+#define NVL_STAMP0() do {} while (0)
+#define NVL_STAMP1() do {} while (0)
+#define NVL_COUNT() do {} while (0)
+#define NVL_STAMP_END() do {} while (0)
 #endif
+
+// ---------------------------------------------------------------------------
+// Scheduler A -- fixed stride, aligned, J == 1 (every chunk a whole buffer;
+// configs 2 and 5).  The workgroup owns a contiguous range of buffers and its
+// 16 waves pull units of U buffers from an LDS counter, so fast and slow waves
+// of a CU finish together (a static per-wave split left the last wave ~20 %
+// behind the mean: older waves win issue arbitration).  U buffers per unit are
+// computed with interleaved chains.
+template <int U>
+__device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
+  NVL_STAMP0();
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t B0 = g.n * blockIdx.x / gridDim.x;
   const uint64_t B1 = g.n * (blockIdx.x + 1) / gridDim.x;
   const uint32_t nunits = (uint32_t)((B1 - B0 + U - 1) / U);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kCtrOff);
 
   auto unit_pos = [&](uint32_t u, int k, Pos& p) -> bool {
     const uint64_t i = B0 + (uint64_t)u * U + (uint64_t)k;
@@ -677,33 +681,27 @@ __device__ __forceinline__ void run_dynamic(const FixedGeom& g, const KArgs& ka,
   uint32_t u = wv;  // first unit pre-assigned; its loads overlap the LDS fill
   Pos gp[U];
   bool ok[U];
-  Piece cur[U];
+  Chunk cur[U];
 #pragma unroll
   for (int k = 0; k < U; ++k) {
     ok[k] = unit_pos(u, k, gp[k]);
-    if (ok[k]) load_piece<true>(gp[k].bi, 0, lane, cur[k]);
+    if (ok[k]) load_chunk<kAligned>(gp[k].bi, 0, lane, cur[k]);
   }
   fill_lds(lds, ka.tables);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
-#if defined(NVL_DIAG_STAMPS)
-  const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime();
-#endif
+  NVL_STAMP1();
 
   while (u < nunits) {
-#if defined(NVL_DIAG_STAMPS)
-    ++nproc;
-#endif
-    uint32_t un = 0;
-    if (lane == 0) un = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    un = __builtin_amdgcn_readfirstlane(un);
+    NVL_COUNT();
+    const uint32_t un = pull_unit(lds, lane);
     Pos np[U];
     bool nok[U];
-    Piece nxt[U];
+    Chunk nxt[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       nok[k] = unit_pos(un, k, np[k]);
-      if (nok[k]) load_piece<true>(np[k].bi, 0, lane, nxt[k]);
+      if (nok[k]) load_chunk<kAligned>(np[k].bi, 0, lane, nxt[k]);
     }
     if (ok[U - 1]) {  // full unit
       BufInfo bis[U];
@@ -713,7 +711,7 @@ __device__ __forceinline__ void run_dynamic(const FixedGeom& g, const KArgs& ka,
         bis[k] = gp[k].bi;
         cs[k] = 0;
       }
-      group_raw<true, U>(lds, lb, bis, cs, lane, cur, raws);
+      group_raw<kAligned, U>(lds, lb, bis, cs, lane, cur, raws);
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < U; ++k) ka.out[gp[k].i] = finish(~raws[k], ka.flags);
@@ -722,7 +720,7 @@ __device__ __forceinline__ void run_dynamic(const FixedGeom& g, const KArgs& ka,
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         if (ok[k]) {
-          const uint32_t r = chunk_raw<true>(lds, lb, gp[k].bi, 0, lane, cur[k]);
+          const uint32_t r = chunk_raw<kAligned>(lds, lb, gp[k].bi, 0, lane, cur[k]);
           if (lane == 0) ka.out[gp[k].i] = finish(~r, ka.flags);
         }
       }
@@ -735,40 +733,131 @@ __device__ __forceinline__ void run_dynamic(const FixedGeom& g, const KArgs& ka,
       cur[k] = nxt[k];
     }
   }
-#if defined(NVL_DIAG_STAMPS)
-  const uint32_t wave = blockIdx.x * kWavesPerWG + wv;
-  if (lane == 0 && wave < 65536) {
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_stamps[4 * wave + 0] = ts0;
-    g_stamps[4 * wave + 1] = ts1;
-    g_stamps[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
-    g_stamps[4 * wave + 3] = ((unsigned long long)xcc << 32) | nproc;
+  NVL_STAMP_END();
+}
+
+// ---------------------------------------------------------------------------
+// Scheduler B -- everything else (any J, any alignment, variable lengths).
+// The chunk space [0, T) is cut into NU = grid * kUnitsPerWG contiguous work
+// units; workgroup b owns units [64b, 64b+64) and its waves pull them from an
+// LDS counter.  A wave walks its unit's chunks in order, accumulating
+// consecutive chunks of one buffer (acc = shift4096(acc) ^ raw); buffers
+// completed inside the unit are written directly, and a buffer cut by a unit
+// boundary leaves a head/tail record for crc32c_fixup_kernel.  The next
+// chunk -- including the first chunk of the next unit -- is always in flight
+// while the current one computes.
+constexpr uint32_t kUnitsPerWG = 64;
+
+template <int M, class G>
+__device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* lds) {
+  NVL_STAMP0();
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t T = g.total();
+  const uint64_t NU = (uint64_t)gridDim.x * kUnitsPerWG;
+  const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
+  auto lo_of = [&](uint32_t uu) -> uint64_t { return T * (uint64_t)uu / NU; };
+
+  // current unit u covers chunks [t, t1); the next unit un is pulled ahead
+  uint32_t u = ub0 + wv;
+  uint64_t t = lo_of(u), t1 = lo_of(u + 1);
+  Pos p{};
+  Chunk cur;
+  bool ready = false;  // p/cur hold chunk t of unit u
+  if (t < t1) {
+    p = unit_start_pos(g, u, t);
+    load_chunk<M>(p.bi, p.c, lane, cur);
+    ready = true;
   }
-#endif
+  fill_lds(lds, ka.tables);
+  __syncthreads();
+  const LaneBase lb = make_lane_base(lane);
+  NVL_STAMP1();
+
+  uint32_t un = ub0 + pull_unit(lds, lane);
+  while (true) {
+    NVL_COUNT();
+    UnitState st{0u, 0u, true, Rec{kNoBuf, 0u, 0u}};
+    Rec tail{kNoBuf, 0u, 0u};
+    if (t < t1) {
+      if (!ready) {
+        p = unit_start_pos(g, u, t);
+        load_chunk<M>(p.bi, p.c, lane, cur);
+      }
+      st.from_zero = (p.c == 0);
+      const uint64_t un_lo = un < ub1 ? lo_of(un) : 0, un_hi = un < ub1 ? lo_of(un + 1) : 0;
+      ready = false;
+      for (; t < t1; ++t) {
+        Pos q = p;
+        Chunk nxt;
+        bool qv = false;
+        if (t + 1 < t1) {
+          q = next_pos(g, p);
+          qv = true;
+        } else if (un_lo < un_hi) {  // first chunk of the next unit
+          q = unit_start_pos(g, un, un_lo);
+          qv = true;
+        }
+        if (M == kGeneral && p.bi.len < 4) {
+          if (qv) load_chunk<M>(q.bi, q.c, lane, nxt);
+          const uint32_t v = tiny_crc(lds, p.bi);
+          if (lane == 0) ka.out[p.i] = finish(v, ka.flags);
+          st.cnt = 0;
+          st.from_zero = true;
+        } else {
+          // Build this chunk's words first (cur dies), then put the next chunk's
+          // loads in flight, then run the chain: the prefetch registers are not
+          // live during the realign/transpose/masking.
+          uint32_t w[16];
+          build_words<M>(p.bi, p.c, lane, cur, w);
+          if (qv) load_chunk<M>(q.bi, q.c, lane, nxt);
+          consume(st, p, chain_fold(lds, lb, w, lane), lds, lane, ka);
+        }
+        if (t + 1 == t1) {
+          if (st.cnt) {
+            if (st.from_zero) tail = Rec{p.i, st.acc, st.cnt};
+            else st.head = Rec{p.i, st.acc, st.cnt};
+          }
+          if (qv) ready = true;  // q is the next unit's first chunk
+        }
+        if (qv) {
+          p = q;
+          cur = nxt;
+        }
+      }
+    }
+    if (ka.recs && lane == 0) {
+      ka.recs[2 * (uint64_t)u] = st.head;
+      ka.recs[2 * (uint64_t)u + 1] = tail;
+    }
+    if (un >= ub1) break;
+    u = un;
+    t = lo_of(u);
+    t1 = lo_of(u + 1);
+    un = ub0 + pull_unit(lds, lane);
+  }
+  NVL_STAMP_END();
 }
 
 #ifndef NVL_FAST_U
-#define NVL_FAST_U 2  // chunks per wave step on the fast path (tools/ab_bench.py: 2 > 1 > 4)
+#define NVL_FAST_U 2  // buffers per unit in scheduler A (tools/ab_bench.py: 2 > 1 > 4)
 #endif
 
-template <bool kFast>
+template <int M>
 __global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-#if !defined(NVL_STATIC_ONLY)
-  if constexpr (kFast) {
+  if constexpr (M == kAligned) {
     if (g.J == 1) {
-      run_dynamic<NVL_FAST_U>(g, ka, lds);
+      run_pairs<NVL_FAST_U>(g, ka, lds);
       return;
     }
   }
-#endif
-  run_waves<kFast, kFast ? NVL_FAST_U : 1>(g, ka, lds);
+  run_units<M>(g, ka, lds);
 }
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  run_waves<false, 1>(g, ka, lds);
+  run_units<kGeneral>(g, ka, lds);
 }
 
 // Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.
@@ -783,8 +872,22 @@ __global__ void crc32c_var_counts(const uint64_t* __restrict__ lengths, uint64_t
   }
 }
 
-// Fold the per-wave records of buffers that straddle waves.  One thread per
-// wave; the wave where a buffer ENDS walks back over earlier waves.
+// unit_first[u] = the buffer holding chunk floor(T*u/NU), T = chunk_start[n]:
+// buffer i owns the units u with cs_i <= floor(T*u/NU) < cs_{i+1}, i.e.
+// u in [ceil(cs_i*NU/T), ceil(cs_{i+1}*NU/T)).
+__global__ void crc32c_unit_map(const uint64_t* __restrict__ cs, uint64_t n, uint64_t NU,
+                                uint64_t* __restrict__ unit_first) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t T = cs[n];
+  const uint64_t a = cs[i], b = cs[i + 1];
+  uint64_t u0 = (a * NU + T - 1) / T, u1 = (b * NU + T - 1) / T;
+  if (u1 > NU) u1 = NU;
+  for (uint64_t u = u0; u < u1; ++u) unit_first[u] = i;
+}
+
+// Fold the per-unit records of buffers cut by work-unit boundaries.  One
+// thread per unit; the unit where a buffer ENDS walks back over earlier units.
 __global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
                                     const uint32_t* __restrict__ tables, uint32_t* __restrict__ out,
                                     uint32_t flags) {
@@ -795,9 +898,9 @@ __global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
   const uint32_t* x2n = tables + kGX2n;
   uint32_t total = h.raw;
   uint64_t after = h.cnt & ~kRecEnds;  // chunks after the current portion
-  // Waves between the buffer's first and last portion either hold a middle
+  // Units between the buffer's first and last portion either hold a middle
   // portion (head record of this buffer) or have an empty chunk range (no
-  // records); the first portion is the tail record of an earlier wave.
+  // records); the first portion is the tail record of an earlier unit.
   for (int64_t x = (int64_t)w - 1; x >= 0; --x) {
     const Rec hx = recs[2 * x];
     if (hx.buf == h.buf) {  // a middle portion
@@ -853,33 +956,42 @@ static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, const uint32
   return hipGetLastError();
 }
 
+static inline uint32_t grid_for(int num_cu, uint64_t T) {
+  uint64_t g = (T + dev::kWavesPerWG - 1) / dev::kWavesPerWG;
+  if (g > (uint64_t)num_cu) g = (uint64_t)num_cu;
+  return g ? (uint32_t)g : 1u;
+}
+
+static inline uint32_t chunks_of(uint64_t len) {
+  return len <= dev::kChunk ? 1u : (uint32_t)((len + dev::kChunk - 1) / dev::kChunk);
+}
+
 hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
                         const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs) {
   if (n == 0) return hipSuccess;
-  const uint32_t J = len <= dev::kChunk ? 1u : (uint32_t)((len + dev::kChunk - 1) / dev::kChunk);
-  const uint64_t T = n * (uint64_t)J;
-  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)lc.num_cu, (T + dev::kWavesPerWG - 1) / dev::kWavesPerWG);
-  if (grid == 0) grid = 1;
-  const bool fast = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
+  const uint32_t J = chunks_of(len);
+  const uint32_t grid = grid_for(lc.num_cu, n * (uint64_t)J);
+  const bool aligned = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
   dev::KArgs ka{out, flags, J > 1 ? recs : nullptr, lc.tables};
-  if (fast)
-    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<true>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  if (aligned)
+    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
+                       ka);
   else
-    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<false>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
+                       ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || J == 1) return e;
-  return launch_fixup(recs, grid * dev::kWavesPerWG, lc.tables, out, flags, lc.stream);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream);
 }
 
-uint32_t fixed_grid(int num_cu, uint64_t len, uint64_t n) {
-  const uint32_t J = len <= dev::kChunk ? 1u : (uint32_t)((len + dev::kChunk - 1) / dev::kChunk);
-  const uint64_t T = n * (uint64_t)J;
-  uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)num_cu, (T + dev::kWavesPerWG - 1) / dev::kWavesPerWG);
-  return grid ? grid : 1;
+size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
+  if (n == 0 || chunks_of(len) == 1) return 0;
+  return 2ull * grid_for(num_cu, n * (uint64_t)chunks_of(len)) * dev::kUnitsPerWG * sizeof(Rec);
 }
 
-uint32_t waves_per_wg() { return dev::kWavesPerWG; }
+size_t var_recs_bytes(int num_cu) { return 2ull * (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(Rec); }
+size_t var_unit_map_bytes(int num_cu) { return (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(uint64_t); }
 
 #if defined(NVL_DIAG_STAMPS)
 extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned long long* host, size_t n) {
@@ -895,16 +1007,21 @@ hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt,
 }
 
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
-                      const uint64_t* chunk_start, uint64_t n, const uint32_t* init, uint32_t init_all,
-                      uint32_t* out, uint32_t flags, Rec* recs) {
+                      const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs) {
   if (n == 0) return hipSuccess;
-  const uint32_t grid = (uint32_t)lc.num_cu;
-  dev::VarGeom g{base, offsets, lengths, chunk_start, n, init, init_all};
+  const uint32_t grid = (uint32_t)lc.num_cu;  // chunk count is only known on the device
+  const uint64_t NU = (uint64_t)grid * dev::kUnitsPerWG;
+  hipLaunchKernelGGL(dev::crc32c_unit_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, lc.stream, chunk_start,
+                     n, NU, unit_first);
+  hipError_t e0 = hipGetLastError();
+  if (e0 != hipSuccess) return e0;
+  dev::VarGeom g{base, offsets, lengths, chunk_start, unit_first, n, init, init_all};
   dev::KArgs ka{out, flags, recs, lc.tables};
   hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_fixup(recs, grid * dev::kWavesPerWG, lc.tables, out, flags, lc.stream);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream);
 }
 
 }  // namespace nvl

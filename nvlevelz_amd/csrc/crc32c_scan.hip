@@ -11,7 +11,7 @@ size_t scan_temp_bytes(uint64_t n) {
   size_t bytes = 0;
   const uint64_t* in = nullptr;
   uint64_t* out = nullptr;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, (hipStream_t)0);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, (hipStream_t)0);
   return bytes;
 }
 

@@ -158,8 +158,22 @@ __device__ __forceinline__ uint32_t slice4_next(const uint8_t* lds, uint32_t x, 
 
 
 
-__device__ __forceinline__ uint32_t comb_lookup(const uint8_t* lds, int lev, int j, uint32_t v) {
-  return lds_u32(lds, kCombOff + ((uint32_t)((lev * 4 + j) << 8) + ((v >> (8 * j)) & 0xFFu)) * 4u);
+// A lane-derived value made opaque at its point of use.  The per-lane table
+// bases below are cheap to recompute; without this the compiler hoists one
+// base per (table, level) out of the main loop, the extra loop-invariant VGPRs
+// spill, and every scratch reload waits (vmcnt) on the in-flight prefetch.
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Byte j of v looked up in 1 KiB table (TAB, j): the lane supplies j through
+// (base = table 0's address for its j, sh = 8j); TAB becomes the ds_read
+// immediate offset.
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t lane_lookup(const uint8_t* lds, uint32_t base, uint32_t sh, uint32_t v) {
+  const uint32_t b = __builtin_amdgcn_ubfe(v, sh, 8);
+  return lds_u32(lds + OFF, base + (b << 2));
 }
 
 // One butterfly level over lane bit LEV: the lane with bit LEV clear holds the
@@ -173,12 +187,14 @@ __device__ __forceinline__ uint32_t fold_level(const uint8_t* lds, uint32_t g, i
   const uint32_t left = hi ? pt : g;
   const uint32_t right = hi ? g : pt;
   uint32_t s;
-  if constexpr (LEV == 0) {
-    const int j = hi ? 2 : 0;
-    s = comb_lookup(lds, TAB, j, left) ^ comb_lookup(lds, TAB, j + 1, left);
+  if constexpr (LEV == 0) {  // lane bit 0 picks bytes {0,1} or {2,3}
+    const uint32_t h = opaque((uint32_t)lane & 1u);
+    const uint32_t base = kCombOff + (h << 11), sh = h << 4;
+    s = lane_lookup<TAB * 4096u>(lds, base, sh, left) ^ lane_lookup<TAB * 4096u + 1024u>(lds, base, sh + 8u, left);
     s ^= dpp_xor1(s);
-  } else {
-    s = comb_lookup(lds, TAB, lane & 3, left);
+  } else {  // lane & 3 picks the byte
+    const uint32_t j = opaque((uint32_t)lane & 3u);
+    s = lane_lookup<TAB * 4096u>(lds, kCombOff + (j << 10), j << 3, left);
     s ^= dpp_xor1(s);
     s ^= dpp_xor2(s);
   }
@@ -198,21 +214,24 @@ __device__ __forceinline__ uint32_t wave_fold(const uint8_t* lds, uint32_t g, in
 
 // shift(acc, 4096) for a wave-uniform acc; every lane gets the result.
 __device__ __forceinline__ uint32_t shift4096(const uint8_t* lds, uint32_t acc, int lane) {
-  const int j = lane & 3;
-  uint32_t s = lds_u32(lds, kShOff + ((uint32_t)(j << 8) + ((acc >> (8 * j)) & 0xFFu)) * 4u);
+  const uint32_t j = opaque((uint32_t)lane & 3u);
+  uint32_t s = lane_lookup<0>(lds, kShOff + (j << 10), j << 3, acc);
   s ^= dpp_xor1(s);
   s ^= dpp_xor2(s);
   return s;
 }
 
 // Fill the LDS image from the device table blob.
+template <int NW>
 __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restrict__ g) {
+  constexpr int kT = kWave * NW;
   const int t = threadIdx.x;
   // replicated slice tables: 8192 16-byte stores, consecutive lanes write
   // consecutive 16 B (conflict-free ds_write_b128).
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint32_t s = (uint32_t)(t + q * kThreads);  // 16-byte slot index
+  for (int q = 0; q < (8192 + kT - 1) / kT; ++q) {
+    const uint32_t s = (uint32_t)(t + q * kT);  // 16-byte slot index
+    if ((8192 % kT) != 0 && s >= 8192u) break;
     const uint32_t off = s << 4;
     const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
     const uint32_t b = (off >> 8) & 0xFFu;
@@ -222,8 +241,8 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restric
   // comb + sh4096 copied verbatim (7168 words = 1792 uint4)
   const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
   uint4* dst = reinterpret_cast<uint4*>(lds + kCombOff);
-  for (int q = t; q < 1792; q += kThreads) dst[q] = src[q];
-  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = (uint32_t)kWavesPerWG;  // units 0..15 are pre-assigned
+  for (int q = t; q < 1792; q += kT) dst[q] = src[q];
+  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = (uint32_t)NW;  // units 0..NW-1 are pre-assigned
 }
 
 __device__ __forceinline__ uint32_t finish(uint32_t crc, uint32_t flags) {
@@ -455,34 +474,32 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
 #else
     if (head) {  // chunk holds the buffer head (or the tail of its ~init)
 #endif
-      const uint32_t P = 16u * (uint32_t)(lane & 3) + (uint32_t)(lane >> 2);
-      const uintptr_t ps = ce - kChunk + 64u * P;
-      int64_t rel = (int64_t)(p - ps);  // bytes of this piece before the buffer
-      rel = rel < -8 ? -8 : (rel > 72 ? 72 : rel);
-      const uint32_t s = bi.s;
+      // d0 = buffer start - chunk start, in (-4, 4096) for a head chunk;
+      // rel = bytes of this lane's piece (P = 16*(lane&3) + (lane>>2)) before
+      // the buffer start.  Word k keeps its bytes at or after the start and
+      // takes the ~init bytes at [rel, rel+4): both from 64-bit shifts whose
+      // clamped amounts make the out-of-range cases come out as 0 / all-ones.
+      const int d0 = (int)(int64_t)(p - (ce - kChunk));
+      const uint32_t l = opaque((uint32_t)lane);
+      const int P = (int)(((l & 3u) << 4) | (l >> 2));
+      const int rel = min(max(d0 - 64 * P, -8), 72);
+      const uint64_t s_hi = (uint64_t)bi.s << 32;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int sh = (int)rel - 4 * k;
-        const uint32_t keep = sh <= 0 ? 0xFFFFFFFFu : (sh >= 4 ? 0u : (0xFFFFFFFFu << (8 * sh)));
-        uint32_t inj = 0;
-        if (sh >= 0 && sh < 4) inj = s << (8 * sh);
-        else if (sh < 0 && sh > -4) inj = s >> (-8 * sh);
+        const int sh = rel - 4 * k;
+        const uint32_t keep = (uint32_t)(~0ull << (8 * min(max(sh, 0), 4)));
+        const uint32_t inj = (uint32_t)(s_hi >> ((32 - 8 * min(max(sh, -4), 4)) & 63));
         w[k] = (w[k] & keep) ^ inj;
       }
     }
   }
 }
 
-// Raw (zero-state, ~init injected) registers of U chunks, wave-uniform.  The
-// U serial slice-by-4 chains and U butterflies are interleaved so each wave
-// keeps U independent LDS round trips in flight.
-template <int M, int U>
-__device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo (&bi)[U],
-                                          const uint32_t (&c)[U], int lane, const Chunk (&ch)[U],
-                                          uint32_t (&raw)[U]) {
-  uint32_t w[U][16];
-#pragma unroll
-  for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u]);
+// Serial slice-by-4 chains + butterflies of U chunks from their built words,
+// interleaved so each wave keeps U independent LDS round trips in flight.
+template <int U>
+__device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16], int lane,
+                                       uint32_t (&raw)[U]) {
   uint32_t crc[U];
 #if defined(NVL_ABL_NOCOMPUTE)  // ablation: keep the loads live, skip every lookup
 #pragma unroll
@@ -519,26 +536,25 @@ __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb
   for (int u = 0; u < U; ++u) raw[u] = crc[u];
 }
 
+// Raw (zero-state, ~init injected) registers of U chunks, wave-uniform.
+template <int M, int U>
+__device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo (&bi)[U],
+                                          const uint32_t (&c)[U], int lane, const Chunk (&ch)[U],
+                                          uint32_t (&raw)[U]) {
+  uint32_t w[U][16];
+#pragma unroll
+  for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u]);
+  chains<U>(lds, lb, w, lane, raw);
+}
+
 // Chain + butterfly of one chunk from its built words.
 __device__ __forceinline__ uint32_t chain_fold(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[16],
                                                int lane) {
-#if defined(NVL_ABL_NOCOMPUTE)
-  uint32_t x = 0;
+  uint32_t w1[1][16], r[1];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) x ^= w[k];
-  return x ^ lane_xor<5>(x);
-#else
-  uint32_t crc = w[0];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) crc = slice4(lds, crc, lb) ^ (k < 15 ? w[k + 1] : 0u);
-  crc = fold_level<0, 4>(lds, crc, lane);
-  crc = fold_level<1, 5>(lds, crc, lane);
-  crc = fold_level<2, 0>(lds, crc, lane);
-  crc = fold_level<3, 1>(lds, crc, lane);
-  crc = fold_level<4, 2>(lds, crc, lane);
-  crc = fold_level<5, 3>(lds, crc, lane);
-  return crc;
-#endif
+  for (int k = 0; k < 16; ++k) w1[0][k] = w[k];
+  chains<1>(lds, lb, w1, lane, r);
+  return r[0];
 }
 
 template <int M>
@@ -636,7 +652,7 @@ __device__ unsigned long long g_stamps[4 * 65536];
 #define NVL_COUNT() (++nproc)
 #define NVL_STAMP_END()                                                                     \
   do {                                                                                      \
-    const uint32_t wave_ = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);                   \
+    const uint32_t wave_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);              \
     if ((threadIdx.x & 63) == 0 && wave_ < 65536) {                                         \
       unsigned xcc_;                                                                        \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
@@ -660,7 +676,7 @@ __device__ unsigned long long g_stamps[4 * 65536];
 // of a CU finish together (a static per-wave split left the last wave ~20 %
 // behind the mean: older waves win issue arbitration).  U buffers per unit are
 // computed with interleaved chains.
-template <int U>
+template <int U, int NW = kWavesPerWG>
 __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
@@ -687,7 +703,7 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
     ok[k] = unit_pos(u, k, gp[k]);
     if (ok[k]) load_chunk<kAligned>(gp[k].bi, 0, lane, cur[k]);
   }
-  fill_lds(lds, ka.tables);
+  fill_lds<NW>(lds, ka.tables);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();
@@ -747,8 +763,12 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
 // chunk -- including the first chunk of the next unit -- is always in flight
 // while the current one computes.
 constexpr uint32_t kUnitsPerWG = 64;
+#ifndef NVL_UNIT_STEP
+#define NVL_UNIT_STEP 1  // chunks per step in scheduler B (2: interleaved pair; A/B'd, no gain)
+#endif
+constexpr int kStep = NVL_UNIT_STEP;
 
-template <int M, class G>
+template <int M, int NW, class G>
 __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
@@ -758,83 +778,107 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
   auto lo_of = [&](uint32_t uu) -> uint64_t { return T * (uint64_t)uu / NU; };
 
-  // current unit u covers chunks [t, t1); the next unit un is pulled ahead
+  // One flat loop over steps.  A step is the next two chunks of the current
+  // unit u (one at an odd tail; none when u is empty), their chains
+  // interleaved.  p0/p1 + c0/c1 hold the step's chunks, loaded while the
+  // previous step computed; the next unit un is pulled ahead so the step that
+  // ends a unit prefetches the next unit's first step.  Every chunk load of the
+  // loop is issued from one place, so the loaded registers carry straight into
+  // the next iteration (no copies that would wait on the loads).
   uint32_t u = ub0 + wv;
   uint64_t t = lo_of(u), t1 = lo_of(u + 1);
-  Pos p{};
-  Chunk cur;
-  bool ready = false;  // p/cur hold chunk t of unit u
-  if (t < t1) {
-    p = unit_start_pos(g, u, t);
-    load_chunk<M>(p.bi, p.c, lane, cur);
-    ready = true;
+  Pos p0{}, p1{};
+  Chunk c0, c1;
+  if (t < t1) {  // the first step's loads overlap the LDS fill
+    p0 = unit_start_pos(g, u, t);
+    load_chunk<M>(p0.bi, p0.c, lane, c0);
+    if (kStep == 2 && t + 1 < t1) {
+      p1 = next_pos(g, p0);
+      load_chunk<M>(p1.bi, p1.c, lane, c1);
+    }
   }
-  fill_lds(lds, ka.tables);
+  fill_lds<NW>(lds, ka.tables);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();
 
   uint32_t un = ub0 + pull_unit(lds, lane);
+  uint64_t un_lo = un < ub1 ? lo_of(un) : 0, un_hi = un < ub1 ? lo_of(un + 1) : 0;
+  UnitState st{0u, 0u, p0.c == 0, Rec{kNoBuf, 0u, 0u}};
+  Rec tail{kNoBuf, 0u, 0u};
   while (true) {
-    NVL_COUNT();
-    UnitState st{0u, 0u, true, Rec{kNoBuf, 0u, 0u}};
-    Rec tail{kNoBuf, 0u, 0u};
-    if (t < t1) {
-      if (!ready) {
-        p = unit_start_pos(g, u, t);
-        load_chunk<M>(p.bi, p.c, lane, cur);
+    const bool cur = t < t1;
+    const bool two = kStep == 2 && t + 1 < t1;
+    const uint64_t tn = cur ? t + (two ? 2u : 1u) : t;
+    const bool unit_ends = tn == t1;
+    Pos q0 = p0, q1 = p0;
+    bool q0v = false, q1v = false;
+    if (!unit_ends) {
+      q0 = two ? next_pos(g, p1) : next_pos(g, p0);
+      q0v = true;
+      if (kStep == 2 && tn + 1 < t1) {
+        q1 = next_pos(g, q0);
+        q1v = true;
       }
-      st.from_zero = (p.c == 0);
-      const uint64_t un_lo = un < ub1 ? lo_of(un) : 0, un_hi = un < ub1 ? lo_of(un + 1) : 0;
-      ready = false;
-      for (; t < t1; ++t) {
-        Pos q = p;
-        Chunk nxt;
-        bool qv = false;
-        if (t + 1 < t1) {
-          q = next_pos(g, p);
-          qv = true;
-        } else if (un_lo < un_hi) {  // first chunk of the next unit
-          q = unit_start_pos(g, un, un_lo);
-          qv = true;
-        }
-        if (M == kGeneral && p.bi.len < 4) {
-          if (qv) load_chunk<M>(q.bi, q.c, lane, nxt);
-          const uint32_t v = tiny_crc(lds, p.bi);
-          if (lane == 0) ka.out[p.i] = finish(v, ka.flags);
-          st.cnt = 0;
-          st.from_zero = true;
-        } else {
-          // Build this chunk's words first (cur dies), then put the next chunk's
-          // loads in flight, then run the chain: the prefetch registers are not
-          // live during the realign/transpose/masking.
-          uint32_t w[16];
-          build_words<M>(p.bi, p.c, lane, cur, w);
-          if (qv) load_chunk<M>(q.bi, q.c, lane, nxt);
-          consume(st, p, chain_fold(lds, lb, w, lane), lds, lane, ka);
-        }
-        if (t + 1 == t1) {
-          if (st.cnt) {
-            if (st.from_zero) tail = Rec{p.i, st.acc, st.cnt};
-            else st.head = Rec{p.i, st.acc, st.cnt};
-          }
-          if (qv) ready = true;  // q is the next unit's first chunk
-        }
-        if (qv) {
-          p = q;
-          cur = nxt;
-        }
+    } else if (un_lo < un_hi) {  // the next unit's first step
+      q0 = unit_start_pos(g, un, un_lo);
+      q0v = true;
+      if (kStep == 2 && un_lo + 1 < un_hi) {
+        q1 = next_pos(g, q0);
+        q1v = true;
       }
     }
-    if (ka.recs && lane == 0) {
-      ka.recs[2 * (uint64_t)u] = st.head;
-      ka.recs[2 * (uint64_t)u + 1] = tail;
+    // Build the words first (c0/c1 die), then put the next step's loads in
+    // flight, then run the chains.
+    uint32_t w[2][16];
+    if (cur) {
+      build_words<M>(p0.bi, p0.c, lane, c0, w[0]);
+      if (two) build_words<M>(p1.bi, p1.c, lane, c1, w[1]);
     }
-    if (un >= ub1) break;
-    u = un;
-    t = lo_of(u);
-    t1 = lo_of(u + 1);
-    un = ub0 + pull_unit(lds, lane);
+    Chunk n0, n1;
+    if (q0v) load_chunk<M>(q0.bi, q0.c, lane, n0);
+    if (q1v) load_chunk<M>(q1.bi, q1.c, lane, n1);
+    if (cur) {
+      NVL_COUNT();
+      uint32_t r[2];
+      if (two) {
+        chains<2>(lds, lb, w, lane, r);
+      } else {
+        r[0] = chain_fold(lds, lb, w[0], lane);
+      }
+      if (M == kGeneral) {  // buffers of < 4 bytes: bytewise, replacing the (unused) chain
+        if (p0.bi.len < 4) r[0] = ~tiny_crc(lds, p0.bi);
+        if (two && p1.bi.len < 4) r[1] = ~tiny_crc(lds, p1.bi);
+      }
+      consume(st, p0, r[0], lds, lane, ka);
+      if (two) consume(st, p1, r[1], lds, lane, ka);
+    }
+    if (unit_ends) {
+      if (st.cnt) {
+        const uint64_t last_i = two ? p1.i : p0.i;  // buffer of the step's last chunk
+        if (st.from_zero) tail = Rec{last_i, st.acc, st.cnt};
+        else st.head = Rec{last_i, st.acc, st.cnt};
+      }
+      if (ka.recs && lane == 0) {
+        ka.recs[2 * (uint64_t)u] = st.head;
+        ka.recs[2 * (uint64_t)u + 1] = tail;
+      }
+      if (un >= ub1) break;
+      u = un;
+      t = un_lo;
+      t1 = un_hi;
+      un = ub0 + pull_unit(lds, lane);
+      un_lo = un < ub1 ? lo_of(un) : 0;
+      un_hi = un < ub1 ? lo_of(un + 1) : 0;
+      st = UnitState{0u, 0u, q0.c == 0, Rec{kNoBuf, 0u, 0u}};
+      tail = Rec{kNoBuf, 0u, 0u};
+    } else {
+      t = tn;
+    }
+    p0 = q0;
+    p1 = q1;
+    c0 = n0;
+    c1 = n1;
   }
   NVL_STAMP_END();
 }
@@ -843,8 +887,15 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
 #define NVL_FAST_U 2  // buffers per unit in scheduler A (tools/ab_bench.py: 2 > 1 > 4)
 #endif
 
+#ifndef NVL_GEN_WAVES
+#define NVL_GEN_WAVES 16  // waves per workgroup of the kGeneral kernels
+#endif
+constexpr int kGenWaves = NVL_GEN_WAVES;
 template <int M>
-__global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
+constexpr int waves_of() { return M == kGeneral ? kGenWaves : kWavesPerWG; }
+
+template <int M>
+__global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   if constexpr (M == kAligned) {
     if (g.J == 1) {
@@ -852,12 +903,12 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_kernel(FixedGeom g, 
       return;
     }
   }
-  run_units<M>(g, ka, lds);
+  run_units<M, waves_of<M>()>(g, ka, lds);
 }
 
-__global__ __launch_bounds__(kThreads, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
+__global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  run_units<kGeneral>(g, ka, lds);
+  run_units<kGeneral, kGenWaves>(g, ka, lds);
 }
 
 // Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.
@@ -978,7 +1029,8 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
     hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
                        ka);
   else
-    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
+    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0,
+                       lc.stream, g,
                        ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || J == 1) return e;
@@ -1018,7 +1070,7 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
   if (e0 != hipSuccess) return e0;
   dev::VarGeom g{base, offsets, lengths, chunk_start, unit_first, n, init, init_all};
   dev::KArgs ka{out, flags, recs, lc.tables};
-  hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0, lc.stream, g, ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream);

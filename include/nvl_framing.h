@@ -1,0 +1,117 @@
+/*
+ * include/nvl_framing.h -- C ABI of the batched call-site shims (SURVEY.md
+ * §8f): the CRC32C framing of LevelDB's on-disk formats computed or checked
+ * for many blocks / records in one GPU batch.  Part of libnvl_crc32c.so.
+ *
+ *   SSTable block trailer  table/format.h:84 (kBlockTrailerSize = 5), written by
+ *                          TableBuilder::WriteRawBlock table/table_builder.cc:175-193,
+ *                          checked by ReadBlock table/format.cc:65-98:
+ *                          block[0..n) | type (1 B) | Mask(Value(block | type)) (LE32)
+ *   Log physical record    db/log_format.h:14-31 (kBlockSize 32768, kHeaderSize 7),
+ *                          written by log::Writer db/log_writer.cc:45-109,
+ *                          parsed by log::Reader::ReadPhysicalRecord db/log_reader.cc:199-281:
+ *                          Mask(Value(type | payload)) (LE32) | len (LE16) | type | payload
+ *
+ * Every entry point computes its CRCs on the GPU (one batch per call) unless
+ * the caller passes NVL_FRAMING_HOST, which selects the host CRC
+ * (nvl_crc32c_extend) explicitly -- for batches too small to pay for a
+ * launch.  There is no implicit fallback: without a usable GPU the device
+ * mode returns the NVL_CRC32C_* error and writes nothing.
+ */
+#ifndef NVL_FRAMING_H_
+#define NVL_FRAMING_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "nvl_crc32c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NVL_FRAMING_HOST 0x100u /* compute CRCs with the host CRC instead of the GPU */
+
+/* ---- SSTable blocks ------------------------------------------------------ */
+
+#define NVL_BLOCK_TRAILER_SIZE 5 /* table/format.h:84 */
+
+/* BlockHandle (table/format.h:22-48): a block of `size` bytes at `offset`,
+ * followed in the file by its 5-byte trailer. */
+typedef struct nvl_block_handle {
+  uint64_t offset;
+  uint64_t size;
+} nvl_block_handle;
+
+/* per-block verdicts of nvl_sstable_verify_blocks, in ReadBlock's order of
+ * checks (table/format.cc:77-135) */
+#define NVL_BLOCK_OK 0
+#define NVL_BLOCK_TRUNCATED 1         /* "truncated block read"      format.cc:82-85 */
+#define NVL_BLOCK_CHECKSUM_MISMATCH 2 /* "block checksum mismatch"   format.cc:88-96 */
+#define NVL_BLOCK_BAD_TYPE 3          /* "bad block type"            format.cc:133-135 */
+
+/* Writer side (replaces the per-block crc32c::Value/Extend/Mask of
+ * table_builder.cc:185-187).  For every handle, file[offset + size] already
+ * holds the block type; writes EncodeFixed32(Mask(Value(file[offset ..
+ * offset+size]))) -- the CRC of block | type -- at file[offset + size + 1].
+ * Every block must lie inside [0, file_len). */
+NVL_API int nvl_sstable_seal_trailers(void* file, uint64_t file_len, const nvl_block_handle* blocks, size_t n,
+                                      uint32_t flags);
+
+/* Reader side (the checksum and type checks of ReadBlock with
+ * verify_checksums, format.cc:77-135, for n blocks at once).  verdict[i]
+ * gets NVL_BLOCK_*; *n_bad (optional) the number of non-OK blocks.  A
+ * compressed block (type 1, kSnappyCompression) verifies as OK here; its
+ * decompression stays with the caller. */
+NVL_API int nvl_sstable_verify_blocks(const void* file, uint64_t file_len, const nvl_block_handle* blocks, size_t n,
+                                      uint8_t* verdict, uint64_t* n_bad, uint32_t flags);
+
+/* ---- log files ----------------------------------------------------------- */
+
+#define NVL_LOG_BLOCK_SIZE 32768 /* db/log_format.h:27 */
+#define NVL_LOG_HEADER_SIZE 7    /* db/log_format.h:30 */
+
+/* Outcome of one ReadPhysicalRecord step (db/log_reader.cc:199-281). */
+#define NVL_LOG_RECORD 0       /* a physical record that passed its checks: payload at offset+7 */
+#define NVL_LOG_BAD_LENGTH 1   /* header length runs past the block: rest of the block dropped,
+                                  "bad record length" (log_reader.cc:234-244) */
+#define NVL_LOG_CHECKSUM 2     /* CRC mismatch: rest of the block dropped, "checksum mismatch"
+                                  (log_reader.cc:254-267) */
+#define NVL_LOG_ZERO 3         /* zero type + zero length (preallocated space): rest of the block
+                                  skipped without a report (log_reader.cc:246-252) */
+#define NVL_LOG_EOF 4          /* end of input, incl. a truncated header or payload in the last
+                                  block, which is not a corruption (log_reader.cc:213-244) */
+
+typedef struct nvl_log_event {
+  uint64_t offset;    /* file offset of the header (RECORD/BAD_LENGTH/CHECKSUM/ZERO) */
+  uint64_t block_end; /* file offset just past the block the event belongs to */
+  uint32_t length;    /* RECORD: payload bytes */
+  uint32_t type;      /* RECORD: the stored type byte (any value; the record-level
+                         state machine reports unknown types) */
+  uint32_t kind;      /* NVL_LOG_* */
+  uint32_t reserved;
+} nvl_log_event;
+
+/* Parse a log image the way log::Reader reads it (32 KiB blocks from
+ * `start`, a multiple of kBlockSize; data[0] is file offset `start`) and
+ * return the sequence of ReadPhysicalRecord outcomes up to and including the
+ * final NVL_LOG_EOF.  `checksum` = 0 skips CRC verification (Reader's
+ * checksum flag).  All candidate records' CRCs (Value(type | payload),
+ * 1 + length bytes) are verified in one batch; a block's records after its
+ * first failure are discarded exactly as the reference drops the block.
+ * `events` may be NULL to query the count: *n_events gets the number of
+ * events; at most `cap` are written; NVL_CRC32C_ENOSPC if cap is too small. */
+NVL_API int nvl_log_scan(const void* data, uint64_t len, uint64_t start, int checksum, nvl_log_event* events,
+                         size_t cap, size_t* n_events, uint32_t flags);
+
+/* Writer side (replaces the per-fragment crc32c::Extend/Mask of
+ * log_writer.cc:93-97): for each header offset, data[off+4..off+7) already
+ * holds length and type; writes EncodeFixed32(Mask(Value(data[off+6 ..
+ * off+7+length)))) at data[off].  One batch for all n records. */
+NVL_API int nvl_log_seal(void* data, uint64_t len, const uint64_t* header_offsets, size_t n, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NVL_FRAMING_H_ */

@@ -1,0 +1,342 @@
+// include/nvl_leveldb_shims.h -- C++ call-site shims of SURVEY.md §8f on top
+// of include/nvl_framing.h: the reference's log::Reader / log::Writer and
+// TableBuilder's block trailers with every CRC of a file computed in one GPU
+// batch.  Header-only, C++11, no LevelDB headers needed: the classes keep the
+// reference's method names and semantics, and INTEGRATION.md shows the
+// adapters (Slice, Status, SequentialFile, WritableFile) for a LevelDB tree.
+//
+//   nvl::shims::LogReader   db/log_reader.h:20-120, db/log_reader.cc:17-281
+//   nvl::shims::LogWriter   db/log_writer.h:18-47, db/log_writer.cc:17-109
+//   nvl::shims::TableFile   TableBuilder::WriteRawBlock table/table_builder.cc:175-193
+//                           + the checks of ReadBlock table/format.cc:65-98
+#ifndef NVL_LEVELDB_SHIMS_H_
+#define NVL_LEVELDB_SHIMS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <string>
+#include <vector>
+
+#include "nvl_framing.h"
+
+namespace nvl {
+namespace shims {
+
+// ---------------------------------------------------------------------------
+// log::Reader over a log image held in memory (the whole file, or its part
+// from block offset 0).  The first ReadRecord scans the image once -- every
+// physical record's checksum in one batch -- and the record-level state
+// machine of log_reader.cc:62-175 then replays the scan.  Corruption reports
+// carry the reference's byte counts and reason strings.
+class LogReader {
+ public:
+  // log_reader.h:22-30 (the reason is the text of the Status::Corruption).
+  class Reporter {
+   public:
+    virtual ~Reporter() {}
+    virtual void Corruption(size_t bytes, const char* reason) = 0;
+  };
+
+  // log_reader.h:32-44.  `file` must stay live while the reader is used;
+  // `flags` may hold NVL_FRAMING_HOST.
+  LogReader(const char* file, uint64_t file_len, Reporter* reporter, bool checksum, uint64_t initial_offset,
+            uint32_t flags = 0)
+      : file_(file),
+        file_len_(file_len),
+        reporter_(reporter),
+        checksum_(checksum),
+        flags_(flags),
+        initial_offset_(initial_offset),
+        resyncing_(initial_offset > 0) {}
+
+  // log_reader.h:46-52.  False at the end of the input, or when the batch
+  // scan failed (status() != NVL_CRC32C_OK; nothing is returned then).
+  bool ReadRecord(const char** data, size_t* size, std::string* scratch) {
+    if (!scanned_) Scan();
+    scratch->clear();
+    *data = "";
+    *size = 0;
+    if (status_ != NVL_CRC32C_OK) return false;
+    bool in_fragmented_record = false;
+    uint64_t prospective_record_offset = 0;
+    const char* frag = "";
+    size_t frag_n = 0;
+    while (true) {
+      const unsigned record_type = ReadPhysicalRecord(&frag, &frag_n);
+      const uint64_t physical_record_offset = pos_ - kHeader - frag_n;
+      if (resyncing_) {  // log_reader.cc:86-95
+        if (record_type == kMiddleType) {
+          continue;
+        } else if (record_type == kLastType) {
+          resyncing_ = false;
+          continue;
+        } else {
+          resyncing_ = false;
+        }
+      }
+      switch (record_type) {
+        case kFullType:
+          if (in_fragmented_record) {
+            if (scratch->empty()) in_fragmented_record = false;
+            else ReportCorruption(scratch->size(), "partial record without end(1)");
+          }
+          prospective_record_offset = physical_record_offset;
+          scratch->clear();
+          *data = frag;
+          *size = frag_n;
+          last_record_offset_ = prospective_record_offset;
+          return true;
+        case kFirstType:
+          if (in_fragmented_record) {
+            if (scratch->empty()) in_fragmented_record = false;
+            else ReportCorruption(scratch->size(), "partial record without end(2)");
+          }
+          prospective_record_offset = physical_record_offset;
+          scratch->assign(frag, frag_n);
+          in_fragmented_record = true;
+          break;
+        case kMiddleType:
+          if (!in_fragmented_record) ReportCorruption(frag_n, "missing start of fragmented record(1)");
+          else scratch->append(frag, frag_n);
+          break;
+        case kLastType:
+          if (!in_fragmented_record) {
+            ReportCorruption(frag_n, "missing start of fragmented record(2)");
+          } else {
+            scratch->append(frag, frag_n);
+            *data = scratch->data();
+            *size = scratch->size();
+            last_record_offset_ = prospective_record_offset;
+            return true;
+          }
+          break;
+        case kEof:
+          if (in_fragmented_record) scratch->clear();
+          return false;
+        case kBadRecord:
+          if (in_fragmented_record) {
+            ReportCorruption(scratch->size(), "error in middle of record");
+            in_fragmented_record = false;
+            scratch->clear();
+          }
+          break;
+        default: {
+          char buf[40];
+          snprintf(buf, sizeof(buf), "unknown record type %u", record_type);
+          ReportCorruption(frag_n + (in_fragmented_record ? scratch->size() : 0), buf);
+          in_fragmented_record = false;
+          scratch->clear();
+          break;
+        }
+      }
+    }
+  }
+
+  // The same for any Slice type with Slice(const char*, size_t).
+  template <class Slice>
+  bool ReadRecord(Slice* record, std::string* scratch) {
+    const char* d;
+    size_t n;
+    const bool ok = ReadRecord(&d, &n, scratch);
+    *record = Slice(d, n);
+    return ok;
+  }
+
+  // log_reader.h:54-58
+  uint64_t LastRecordOffset() const { return last_record_offset_; }
+
+  int status() const { return status_; }
+
+ private:
+  enum : unsigned { kZeroType = 0, kFullType = 1, kFirstType = 2, kMiddleType = 3, kLastType = 4 };
+  enum : unsigned { kEof = kLastType + 1, kBadRecord = kLastType + 2 };  // log_reader.h:84-92
+  static const uint64_t kBlock = NVL_LOG_BLOCK_SIZE;
+  static const uint64_t kHeader = NVL_LOG_HEADER_SIZE;
+
+  // SkipToInitialBlock (log_reader.cc:36-60), then the one batch scan.
+  void Scan() {
+    scanned_ = true;
+    uint64_t in_block = initial_offset_ % kBlock;
+    uint64_t block_start = initial_offset_ - in_block;
+    if (in_block > kBlock - 6) block_start += kBlock;  // don't search a block if we'd be in the trailer
+    pos_ = block_start;
+    next_ = 0;
+    if (block_start >= file_len_) {  // skipped to (or past) the end: the first read finds nothing
+      nvl_log_event eof = {block_start, block_start, 0u, 0u, NVL_LOG_EOF, 0u};
+      events_.assign(1, eof);
+      return;
+    }
+    const uint64_t n = file_len_ - block_start;
+    size_t ne = 0;
+    const size_t cap = (size_t)(n / kHeader + n / kBlock + 4);  // bound on the event count
+    events_.resize(cap);
+    status_ = nvl_log_scan(file_ + block_start, n, block_start, checksum_ ? 1 : 0, events_.data(), cap, &ne, flags_);
+    events_.resize(status_ == NVL_CRC32C_OK ? ne : 0);
+  }
+
+  // ReadPhysicalRecord (log_reader.cc:199-281) replayed from the scan.
+  // pos_ mirrors end_of_buffer_offset_ - buffer_.size().
+  unsigned ReadPhysicalRecord(const char** frag, size_t* frag_n) {
+    if (next_ >= events_.size()) return kEof;
+    const nvl_log_event& e = events_[next_];
+    switch (e.kind) {
+      case NVL_LOG_RECORD:
+        ++next_;
+        pos_ = e.offset + kHeader + e.length;
+        if (e.offset < initial_offset_) {  // started before initial_offset_ (:270-275)
+          *frag = "";
+          *frag_n = 0;
+          return kBadRecord;
+        }
+        *frag = file_ + e.offset + kHeader;
+        *frag_n = e.length;
+        return e.type;
+      case NVL_LOG_BAD_LENGTH:
+        ++next_;
+        pos_ = e.block_end;
+        ReportCorruption(e.block_end - e.offset, "bad record length");
+        return kBadRecord;
+      case NVL_LOG_CHECKSUM:
+        ++next_;
+        pos_ = e.block_end;
+        ReportCorruption(e.block_end - e.offset, "checksum mismatch");
+        return kBadRecord;
+      case NVL_LOG_ZERO:
+        ++next_;
+        pos_ = e.block_end;
+        return kBadRecord;
+      default:  // NVL_LOG_EOF: stays at the end
+        pos_ = e.block_end;
+        return kEof;
+    }
+  }
+
+  // ReportCorruption / ReportDrop (log_reader.cc:181-190), unsigned arithmetic as there.
+  void ReportCorruption(uint64_t bytes, const char* reason) {
+    if (reporter_ != nullptr && pos_ - bytes >= initial_offset_) reporter_->Corruption((size_t)bytes, reason);
+  }
+
+  const char* const file_;
+  const uint64_t file_len_;
+  Reporter* const reporter_;
+  const bool checksum_;
+  const uint32_t flags_;
+  const uint64_t initial_offset_;
+  bool resyncing_;
+  bool scanned_ = false;
+  int status_ = NVL_CRC32C_OK;
+  std::vector<nvl_log_event> events_;
+  size_t next_ = 0;
+  uint64_t pos_ = 0;
+  uint64_t last_record_offset_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// log::Writer that stages physical records (fragmentation and block trailers
+// exactly as log_writer.cc:36-82) and seals all their headers in one batch
+// when the bytes are taken.  Byte-identical output to the reference writer.
+class LogWriter {
+ public:
+  // log_writer.h:22-30: a writer appending to a file of dest_length bytes.
+  explicit LogWriter(uint64_t dest_length = 0) : block_offset_(dest_length % NVL_LOG_BLOCK_SIZE) {}
+
+  // log_writer.cc:36-82.
+  void AddRecord(const char* ptr, size_t left) {
+    bool begin = true;
+    do {
+      const uint64_t leftover = kBlock - block_offset_;
+      if (leftover < kHeader) {  // switch to a new block, zero-filling the trailer
+        buf_.append((size_t)leftover, '\0');
+        block_offset_ = 0;
+      }
+      const size_t avail = (size_t)(kBlock - block_offset_ - kHeader);
+      const size_t fragment_length = left < avail ? left : avail;
+      const bool end = left == fragment_length;
+      const unsigned type = begin && end ? 1u : begin ? 2u : end ? 4u : 3u;  // Full, First, Last, Middle
+      EmitPhysicalRecord(type, ptr, fragment_length);
+      ptr += fragment_length;
+      left -= fragment_length;
+      begin = false;
+    } while (left > 0);
+  }
+
+  // Seal every staged header (one batch) and move the bytes into *out.
+  int Take(std::string* out, uint32_t flags = 0) {
+    const int rc = nvl_log_seal(&buf_[0], buf_.size(), headers_.data(), headers_.size(), flags);
+    if (rc != NVL_CRC32C_OK) return rc;
+    out->append(buf_);
+    buf_.clear();
+    headers_.clear();
+    return NVL_CRC32C_OK;
+  }
+
+  size_t pending_bytes() const { return buf_.size(); }
+  size_t pending_records() const { return headers_.size(); }
+
+ private:
+  static const uint64_t kBlock = NVL_LOG_BLOCK_SIZE;
+  static const uint64_t kHeader = NVL_LOG_HEADER_SIZE;
+
+  // log_writer.cc:84-109 with the CRC left for Take().
+  void EmitPhysicalRecord(unsigned t, const char* ptr, size_t n) {
+    headers_.push_back(buf_.size());
+    const char h[NVL_LOG_HEADER_SIZE] = {0, 0, 0, 0, (char)(n & 0xff), (char)(n >> 8), (char)t};
+    buf_.append(h, kHeader);
+    buf_.append(ptr, n);
+    block_offset_ += kHeader + n;
+  }
+
+  uint64_t block_offset_;
+  std::string buf_;
+  std::vector<uint64_t> headers_;
+};
+
+// ---------------------------------------------------------------------------
+// An SSTable being written: TableBuilder appends raw bytes and blocks here
+// instead of to its WritableFile; block offsets never depend on CRC values
+// (fixed 5-byte trailer), so the trailers are sealed in one batch when the
+// image is complete (TableBuilder::Finish, table_builder.cc:199-253).
+class TableFile {
+ public:
+  void Append(const char* data, size_t n) { image_.append(data, n); }
+
+  // WriteRawBlock (table_builder.cc:175-193) with the CRC deferred: returns
+  // the BlockHandle {offset, size}.
+  nvl_block_handle AppendBlock(const char* contents, size_t n, uint8_t type) {
+    nvl_block_handle h{image_.size(), n};
+    image_.append(contents, n);
+    const char trailer[NVL_BLOCK_TRAILER_SIZE] = {(char)type, 0, 0, 0, 0};
+    image_.append(trailer, NVL_BLOCK_TRAILER_SIZE);
+    blocks_.push_back(h);
+    return h;
+  }
+
+  // All trailers in one batch; the image is then byte-identical to the
+  // reference builder's file.
+  int Seal(uint32_t flags = 0) {
+    return nvl_sstable_seal_trailers(&image_[0], image_.size(), blocks_.data(), blocks_.size(), flags);
+  }
+
+  uint64_t size() const { return image_.size(); }
+  const std::string& image() const { return image_; }
+  const std::vector<nvl_block_handle>& blocks() const { return blocks_; }
+
+ private:
+  std::string image_;
+  std::vector<nvl_block_handle> blocks_;
+};
+
+// ReadBlock's checks (format.cc:77-135) for every block of a table image in
+// one batch; verdict[i] = NVL_BLOCK_*.  Returns the batch status.
+inline int VerifyBlocks(const char* file, uint64_t file_len, const std::vector<nvl_block_handle>& blocks,
+                        std::vector<uint8_t>* verdict, uint64_t* n_bad, uint32_t flags = 0) {
+  verdict->assign(blocks.size(), NVL_BLOCK_OK);
+  return nvl_sstable_verify_blocks(file, file_len, blocks.data(), blocks.size(), verdict->data(), n_bad, flags);
+}
+
+}  // namespace shims
+}  // namespace nvl
+
+#endif  // NVL_LEVELDB_SHIMS_H_

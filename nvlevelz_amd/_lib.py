@@ -14,7 +14,9 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnvl_crc32c.so")
-HEADER = os.path.join(os.path.dirname(HERE), "include", "nvl_crc32c.h")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+HEADER = os.path.join(INCLUDE, "nvl_crc32c.h")
+HEADERS = [HEADER, os.path.join(INCLUDE, "nvl_framing.h")]
 
 OK = 0
 EINVAL = -1
@@ -49,14 +51,32 @@ SIGNATURES = {
     "nvl_crc32c_batch_host": (_int, [_vp, _vp, _vp, _u32, _vp, _u64, _u32]),
     "nvl_crc32c_fixed_host": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _u32]),
     "nvl_crc32c_fill_splitmix": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
+    "nvl_crc32c_batch_region_host": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32]),
+    # include/nvl_framing.h
+    "nvl_sstable_seal_trailers": (_int, [_vp, _u64, _vp, _sz, _u32]),
+    "nvl_sstable_verify_blocks": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _u32]),
+    "nvl_log_scan": (_int, [_vp, _u64, _u64, _int, _vp, _sz, _vp, _u32]),
+    "nvl_log_seal": (_int, [_vp, _u64, _vp, _sz, _u32]),
 }
 
+FRAMING_HOST = 0x100
+BLOCK_OK, BLOCK_TRUNCATED, BLOCK_CHECKSUM_MISMATCH, BLOCK_BAD_TYPE = 0, 1, 2, 3
+LOG_RECORD, LOG_BAD_LENGTH, LOG_CHECKSUM, LOG_ZERO, LOG_EOF = 0, 1, 2, 3, 4
 
-def header_symbols(path: str = HEADER) -> list[str]:
-    """Every entry point the C header declares (NVL_API ... nvl_crc32c_x(...))."""
-    with open(path) as f:
-        text = f.read()
-    return sorted(set(re.findall(r"NVL_API[^;(]*?\b(nvl_crc32c_\w+)\s*\(", text)))
+
+class LogEvent(ctypes.Structure):
+    """nvl_log_event (include/nvl_framing.h)."""
+    _fields_ = [("offset", _u64), ("block_end", _u64), ("length", _u32), ("type", _u32),
+                ("kind", _u32), ("reserved", _u32)]
+
+
+def header_symbols(paths: list[str] | None = None) -> list[str]:
+    """Every entry point the C headers declare (NVL_API ... nvl_x(...))."""
+    names: set[str] = set()
+    for path in paths or HEADERS:
+        with open(path) as f:
+            names |= set(re.findall(r"NVL_API[^;(]*?\b(nvl_\w+)\s*\(", f.read()))
+    return sorted(names)
 
 
 def load() -> ctypes.CDLL:

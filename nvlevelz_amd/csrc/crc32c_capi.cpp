@@ -162,13 +162,18 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   uint64_t* unit_first = reinterpret_cast<uint64_t*>(w + off_map);
   Rec* recs = reinterpret_cast<Rec*>(w + off_recs);
   void* tmp = w + off_tmp;
-  hipError_t e = launch_var_counts(lengths, n, cnt, st);
-  if (e == hipSuccess) e = exclusive_scan_u64(tmp, need - off_tmp, cnt, cs, n + 1, st);
-  if (e == hipSuccess) {
-    LaunchCtx lc{st, s->num_cu, s->tables};
-    e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, unit_first, n, init, init_all, out,
-                   flags, recs);
+  LaunchCtx lc{st, s->num_cu, s->tables};
+  const bool small = var_plan_small(n);
+  hipError_t e;
+  if (small) {
+    e = launch_var_plan_small(lc, lengths, n, cs, unit_first);
+  } else {
+    e = launch_var_counts(lengths, n, cnt, st);
+    if (e == hipSuccess) e = exclusive_scan_u64(tmp, need - off_tmp, cnt, cs, n + 1, st);
   }
+  if (e == hipSuccess)
+    e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, unit_first, n, init, init_all, out,
+                   flags, recs, small);
   if (own) (void)hipFreeAsync(ws, st);
   return hip_rc(e);
 }
@@ -387,6 +392,60 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   size_t off_cs, off_map, off_recs, off_tmp;
   const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_tmp);
   const size_t dbytes = total + n * 4 + ws + 512;
+  if (hipMallocAsync(&d, dbytes, st) != hipSuccess) {
+    (void)hipStreamDestroy(st);
+    return NVL_CRC32C_EHIP;
+  }
+  uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
+  void* dws = d + align_up(total, 256) + align_up(n * 4, 256);
+  hipError_t e = hipMemcpyAsync(d, hst, total, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
+                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);
+  else
+    rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
+  (void)hipFreeAsync(d, st);
+  if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  (void)hipStreamDestroy(st);
+  return rc;
+}
+
+int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const uint64_t* offsets,
+                                 const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
+                                 uint64_t n, uint32_t flags) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!offsets || !lengths || !out || (!region && region_len)) return NVL_CRC32C_EINVAL;
+  uint64_t lo = UINT64_MAX, hi = 0;  // staged window [lo, hi)
+  for (uint64_t i = 0; i < n; ++i) {
+    if (lengths[i] > region_len || offsets[i] > region_len - lengths[i]) return NVL_CRC32C_EINVAL;
+    if (offsets[i] < lo) lo = offsets[i];
+    if (offsets[i] + lengths[i] > hi) hi = offsets[i] + lengths[i];
+  }
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  if (!s) return rc;
+  // host layout: [window bytes] [offsets n (rebased to the window)] [lengths n] [init n]
+  const uint64_t wbytes = hi - lo;
+  const size_t meta_off = align_up(wbytes, 256);
+  const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
+  uint8_t* hst = static_cast<uint8_t*>(t_staging.get(total));
+  if (!hst) return NVL_CRC32C_EHIP;
+  memcpy(hst, static_cast<const uint8_t*>(region) + lo, wbytes);
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(hst + meta_off);
+  uint64_t* hlen = hoff + n;
+  uint32_t* hini = reinterpret_cast<uint32_t*>(hlen + n);
+  for (uint64_t i = 0; i < n; ++i) {
+    hoff[i] = offsets[i] - lo;
+    hlen[i] = lengths[i];
+    hini[i] = init ? init[i] : init_all;
+  }
+  hipStream_t st;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
+  uint8_t* d = nullptr;
+  size_t off_cs, off_map, off_recs, off_tmp;
+  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_tmp);
+  const size_t dbytes = align_up(total, 256) + align_up(n * 4, 256) + ws + 256;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) {
     (void)hipStreamDestroy(st);
     return NVL_CRC32C_EHIP;

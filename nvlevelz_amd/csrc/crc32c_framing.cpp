@@ -1,0 +1,242 @@
+// nvlevelz_amd/csrc/crc32c_framing.cpp -- the batched call-site shims of
+// SURVEY.md §8f behind include/nvl_framing.h: SSTable block trailers
+// (table/table_builder.cc:175-193 / table/format.cc:65-98) and log physical
+// records (db/log_writer.cc:84-109 / db/log_reader.cc:199-281).  The framing
+// logic is host code; every CRC of a call goes to the GPU in ONE batch
+// (nvl_crc32c_batch_region_host) unless NVL_FRAMING_HOST asks for the host
+// CRC explicitly.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "crc32c_internal.h"
+#include "crc32c_math.h"
+#include "nvl_framing.h"
+
+namespace nvl {
+namespace {
+
+inline uint32_t load_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+inline void store_le32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  p[2] = (uint8_t)(v >> 16);
+  p[3] = (uint8_t)(v >> 24);
+}
+
+// crc[i] = Value(region[off[i] .. off[i]+len[i])): one GPU batch, or the host
+// CRC when the caller selected it.
+int value_many(const uint8_t* region, uint64_t region_len, const std::vector<uint64_t>& off,
+               const std::vector<uint64_t>& len, std::vector<uint32_t>* crc, uint32_t flags) {
+  const size_t n = off.size();
+  crc->assign(n, 0u);
+  if (n == 0) return NVL_CRC32C_OK;
+  if (flags & NVL_FRAMING_HOST) {
+    for (size_t i = 0; i < n; ++i) (*crc)[i] = host_extend(0, region + off[i], len[i]);
+    return NVL_CRC32C_OK;
+  }
+  return nvl_crc32c_batch_region_host(region, region_len, off.data(), len.data(), nullptr, 0, crc->data(), n, 0);
+}
+
+bool block_in_file(const nvl_block_handle& h, uint64_t file_len) {
+  return h.size <= file_len && h.offset <= file_len - h.size &&
+         file_len - h.size - h.offset >= (uint64_t)NVL_BLOCK_TRAILER_SIZE;
+}
+
+constexpr uint64_t kLogBlock = NVL_LOG_BLOCK_SIZE;
+constexpr uint64_t kLogHeader = NVL_LOG_HEADER_SIZE;
+
+// One block's speculative parse: every candidate record is assumed to pass
+// its checksum; the block's closing event (if any) is what the parse reached
+// under that assumption.
+struct BlockParse {
+  uint64_t start, end;      // file offsets of the block bytes read
+  size_t first, count;      // candidate records: cand[first .. first+count)
+  nvl_log_event closing;    // BAD_LENGTH / ZERO / EOF, or kind = UINT32_MAX (none: trailer skipped)
+};
+
+}  // namespace
+}  // namespace nvl
+
+using namespace nvl;
+
+extern "C" {
+
+int nvl_sstable_seal_trailers(void* file, uint64_t file_len, const nvl_block_handle* blocks, size_t n,
+                              uint32_t flags) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!file || !blocks) return NVL_CRC32C_EINVAL;
+  std::vector<uint64_t> off(n), len(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (!block_in_file(blocks[i], file_len)) return NVL_CRC32C_EINVAL;
+    off[i] = blocks[i].offset;
+    len[i] = blocks[i].size + 1;  // block contents | type (table_builder.cc:185-186)
+  }
+  uint8_t* f = static_cast<uint8_t*>(file);
+  std::vector<uint32_t> crc;
+  const int rc = value_many(f, file_len, off, len, &crc, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+  for (size_t i = 0; i < n; ++i) store_le32(f + blocks[i].offset + blocks[i].size + 1, mask(crc[i]));  // :187
+  return NVL_CRC32C_OK;
+}
+
+int nvl_sstable_verify_blocks(const void* file, uint64_t file_len, const nvl_block_handle* blocks, size_t n,
+                              uint8_t* verdict, uint64_t* n_bad, uint32_t flags) {
+  if (n_bad) *n_bad = 0;
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!file || !blocks || !verdict) return NVL_CRC32C_EINVAL;
+  const uint8_t* f = static_cast<const uint8_t*>(file);
+  std::vector<uint64_t> off, len;
+  std::vector<size_t> which;
+  off.reserve(n);
+  len.reserve(n);
+  which.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (!block_in_file(blocks[i], file_len)) continue;  // "truncated block read" (format.cc:82-85)
+    off.push_back(blocks[i].offset);
+    len.push_back(blocks[i].size + 1);
+    which.push_back(i);
+  }
+  std::vector<uint32_t> crc;
+  const int rc = value_many(f, file_len, off, len, &crc, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+  for (size_t i = 0; i < n; ++i) verdict[i] = NVL_BLOCK_TRUNCATED;
+  for (size_t k = 0; k < which.size(); ++k) {
+    const nvl_block_handle& h = blocks[which[k]];
+    const uint8_t* trailer = f + h.offset + h.size;
+    uint8_t v = NVL_BLOCK_OK;
+    if (crc[k] != unmask(load_le32(trailer + 1))) v = NVL_BLOCK_CHECKSUM_MISMATCH;  // format.cc:88-96
+    else if (trailer[0] != 0 && trailer[0] != 1) v = NVL_BLOCK_BAD_TYPE;           // format.cc:98-135
+    verdict[which[k]] = v;
+  }
+  if (n_bad) {
+    uint64_t b = 0;
+    for (size_t i = 0; i < n; ++i) b += verdict[i] != NVL_BLOCK_OK;
+    *n_bad = b;
+  }
+  return NVL_CRC32C_OK;
+}
+
+int nvl_log_scan(const void* data, uint64_t len, uint64_t start, int checksum, nvl_log_event* events, size_t cap,
+                 size_t* n_events, uint32_t flags) {
+  if (n_events) *n_events = 0;
+  if ((!data && len) || !n_events || (start % kLogBlock) != 0) return NVL_CRC32C_EINVAL;
+  const uint8_t* d = static_cast<const uint8_t*>(data);
+
+  // Pass 1: speculative parse of every block (ReadPhysicalRecord's header
+  // checks, log_reader.cc:203-252), collecting candidate records.
+  std::vector<BlockParse> blocks;
+  std::vector<nvl_log_event> cand;
+  std::vector<uint64_t> coff, clen;
+  uint64_t b0 = 0;
+  while (true) {
+    // log::Reader reads kBlockSize at a time; a short read (incl. 0 bytes)
+    // marks EOF (log_reader.cc:205-218).
+    const uint64_t m = (len - b0) < kLogBlock ? (len - b0) : kLogBlock;
+    const bool eof = m < kLogBlock;
+    BlockParse bp{start + b0, start + b0 + m, cand.size(), 0, nvl_log_event{}};
+    bp.closing.kind = UINT32_MAX;
+    uint64_t pos = 0;
+    while (true) {
+      nvl_log_event e{start + b0 + pos, bp.end, 0u, 0u, 0u, 0u};
+      if (m - pos < kLogHeader) {
+        if (eof) {  // empty, or a truncated header at the end of the file: EOF, not a corruption
+          e.kind = NVL_LOG_EOF;
+          bp.closing = e;
+        }
+        break;  // otherwise the block trailer is skipped
+      }
+      const uint8_t* h = d + b0 + pos;
+      const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+      const uint32_t type = h[6];
+      if (kLogHeader + length > m - pos) {
+        e.kind = eof ? NVL_LOG_EOF : NVL_LOG_BAD_LENGTH;  // :234-244
+        bp.closing = e;
+        break;
+      }
+      if (type == 0 && length == 0) {  // :246-252
+        e.kind = NVL_LOG_ZERO;
+        bp.closing = e;
+        break;
+      }
+      e.kind = NVL_LOG_RECORD;
+      e.length = length;
+      e.type = type;
+      cand.push_back(e);
+      coff.push_back(b0 + pos + 6);  // Value(header + 6, 1 + length): type | payload (:256-257)
+      clen.push_back(1u + length);
+      ++bp.count;
+      pos += kLogHeader + length;
+    }
+    blocks.push_back(bp);
+    if (eof) break;
+    b0 += kLogBlock;
+  }
+
+  // Pass 2: every candidate's CRC in one batch.
+  std::vector<uint32_t> crc;
+  if (checksum) {
+    const int rc = value_many(d, len, coff, clen, &crc, flags);
+    if (rc != NVL_CRC32C_OK) return rc;
+  }
+
+  // Pass 3: replay in reader order; a block is cut at its first mismatch
+  // (the rest of the buffer is dropped, log_reader.cc:258-266).
+  size_t ne = 0;
+  auto emit = [&](const nvl_log_event& e) {
+    if (events && ne < cap) events[ne] = e;
+    ++ne;
+  };
+  for (const BlockParse& bp : blocks) {
+    bool cut = false;
+    for (size_t k = bp.first; k < bp.first + bp.count; ++k) {
+      const nvl_log_event& e = cand[k];
+      if (checksum && crc[k] != unmask(load_le32(d + (e.offset - start)))) {
+        nvl_log_event x = e;
+        x.kind = NVL_LOG_CHECKSUM;
+        x.length = 0;
+        x.type = 0;
+        emit(x);
+        cut = true;
+        break;
+      }
+      emit(e);
+    }
+    if (!cut && bp.closing.kind != UINT32_MAX) emit(bp.closing);
+    const bool eof_block = bp.end - bp.start < kLogBlock;
+    if (eof_block && (cut || bp.closing.kind != NVL_LOG_EOF)) {
+      // a drop or zero record emptied the last buffer: the next read finds nothing
+      nvl_log_event x{bp.end, bp.end, 0u, 0u, NVL_LOG_EOF, 0u};
+      emit(x);
+    }
+  }
+  *n_events = ne;
+  if (events && ne > cap) return NVL_CRC32C_ENOSPC;
+  return NVL_CRC32C_OK;
+}
+
+int nvl_log_seal(void* data, uint64_t len, const uint64_t* header_offsets, size_t n, uint32_t flags) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!data || !header_offsets) return NVL_CRC32C_EINVAL;
+  uint8_t* d = static_cast<uint8_t*>(data);
+  std::vector<uint64_t> off(n), ln(n);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t o = header_offsets[i];
+    if (o > len || len - o < kLogHeader) return NVL_CRC32C_EINVAL;
+    const uint64_t length = (uint64_t)d[o + 4] | ((uint64_t)d[o + 5] << 8);
+    if (len - o - kLogHeader < length) return NVL_CRC32C_EINVAL;
+    off[i] = o + 6;  // type | payload (log_writer.cc:93-94)
+    ln[i] = 1 + length;
+  }
+  std::vector<uint32_t> crc;
+  const int rc = value_many(d, len, off, ln, &crc, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+  for (size_t i = 0; i < n; ++i) store_le32(d + header_offsets[i], mask(crc[i]));  // :95-96
+  return NVL_CRC32C_OK;
+}
+
+}  // extern "C"

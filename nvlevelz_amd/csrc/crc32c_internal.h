@@ -40,10 +40,16 @@ size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n);  // workspace of 
 size_t var_recs_bytes(int num_cu);                               // record part of launch_var's workspace
 size_t var_unit_map_bytes(int num_cu);                           // unit map part of launch_var's workspace
 
+// Plan for the variable-length kernel: small batches in one launch
+// (chunk_start + unit map), large ones as counts -> device scan -> unit map.
+bool var_plan_small(uint64_t n);
+hipError_t launch_var_plan_small(const LaunchCtx& lc, const uint64_t* lengths, uint64_t n, uint64_t* chunk_start,
+                                 uint64_t* unit_first);
 hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st);
+// have_unit_map: unit_first already written (small plan); otherwise built here.
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
-                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs);
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, bool have_unit_map);
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

@@ -516,7 +516,7 @@ __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, c
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) crc[u] = slice4(lds, crc[u], lb) ^ (k < 15 ? w[u][k + 1] : 0u);
+    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
   }
   // Lane -> stream position P = 16*(lane&3) + (lane>>2): lane bits 0,1 step
   // 1024/2048 bytes (comb tables 4, 5), bits 2..5 step 64..512 (tables 0..3).
@@ -937,6 +937,75 @@ __global__ void crc32c_unit_map(const uint64_t* __restrict__ cs, uint64_t n, uin
   for (uint64_t u = u0; u < u1; ++u) unit_first[u] = i;
 }
 
+// ceil(a / d) for a < 2^62, d > 0: a double-precision estimate corrected by
+// at most a step or two (a full 64-bit division is a long software loop).
+__device__ __forceinline__ uint64_t ceil_div_u64(uint64_t a, uint64_t d) {
+  uint64_t q = (uint64_t)((double)a / (double)d);
+  while (q * d < a) ++q;
+  while (q > 0 && (q - 1) * d >= a) --q;
+  return q;
+}
+
+// The whole variable-length plan in one workgroup, for batches of up to
+// kPlanSmallMax buffers: chunk counts, their exclusive prefix (chunk_start,
+// cs[n] = T) and the unit map -- one launch instead of counts + device scan +
+// unit map.  The chunk counts are staged in LDS by one fully parallel,
+// coalesced pass; the prefix is then scanned tile by tile (1024 buffers, thread
+// t holding buffer 1024k + t) out of LDS.
+constexpr uint64_t kPlanThreads = 1024;
+constexpr uint64_t kPlanSmallMax = 32768;
+
+__global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t* __restrict__ lengths, uint64_t n,
+                                                                uint64_t NU, uint64_t* __restrict__ cs,
+                                                                uint64_t* __restrict__ unit_first) {
+  __shared__ uint32_t js[kPlanSmallMax];  // chunk counts (a buffer of < 2^40 bytes has < 2^28 chunks)
+  __shared__ uint64_t wsum[kPlanThreads / kWave];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t nn = (uint32_t)n;
+#pragma unroll 8
+  for (uint32_t i = t; i < nn; i += kPlanThreads) {
+    const uint64_t L = lengths[i];
+    js[i] = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
+  }
+  __syncthreads();
+  uint64_t carry = 0;
+#pragma unroll 1
+  for (uint32_t base = 0; base < nn; base += kPlanThreads) {
+    const uint32_t i = base + t;
+    const uint32_t j = i < nn ? js[i] : 0u;
+    uint64_t x = j;  // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t before = 0, tile = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < kPlanThreads / kWave; ++v) {
+      const uint64_t sv = wsum[v];
+      before += v < wv ? sv : 0;
+      tile += sv;
+    }
+    if (i < nn) cs[i] = carry + before + x - j;
+    carry += tile;
+    __syncthreads();  // wsum is reused by the next tile
+  }
+  const uint64_t T = carry;
+  if (t == 0) cs[n] = T;
+  // Unit map: buffer i owns the units u with cs_i <= floor(T*u/NU) < cs_i + J_i,
+  // i.e. u in [ceil(cs_i*NU/T), ceil((cs_i+J_i)*NU/T)) (see crc32c_unit_map);
+  // cs_i is read back from this thread's own store.
+  for (uint32_t i = t; i < nn; i += kPlanThreads) {
+    const uint64_t c0 = cs[i];
+    const uint64_t u0 = ceil_div_u64(c0 * NU, T);
+    uint64_t u1 = ceil_div_u64((c0 + js[i]) * NU, T);
+    if (u1 > NU) u1 = NU;
+    for (uint64_t u = u0; u < u1; ++u) unit_first[u] = i;
+  }
+}
+
 // Fold the per-unit records of buffers cut by work-unit boundaries.  One
 // thread per unit; the unit where a buffer ENDS walks back over earlier units.
 __global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
@@ -1051,6 +1120,16 @@ extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned l
 }
 #endif
 
+bool var_plan_small(uint64_t n) { return n <= dev::kPlanSmallMax; }
+
+hipError_t launch_var_plan_small(const LaunchCtx& lc, const uint64_t* lengths, uint64_t n, uint64_t* chunk_start,
+                                 uint64_t* unit_first) {
+  const uint64_t NU = (uint64_t)lc.num_cu * dev::kUnitsPerWG;
+  hipLaunchKernelGGL(dev::crc32c_plan_small, dim3(1), dim3((uint32_t)dev::kPlanThreads), 0, lc.stream, lengths, n, NU,
+                     chunk_start, unit_first);
+  return hipGetLastError();
+}
+
 hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st) {
   const uint32_t tpb = 256;
   const uint64_t blocks = (n + 1 + tpb - 1) / tpb;
@@ -1060,14 +1139,16 @@ hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt,
 
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
-                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs) {
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, bool have_unit_map) {
   if (n == 0) return hipSuccess;
   const uint32_t grid = (uint32_t)lc.num_cu;  // chunk count is only known on the device
   const uint64_t NU = (uint64_t)grid * dev::kUnitsPerWG;
-  hipLaunchKernelGGL(dev::crc32c_unit_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, lc.stream, chunk_start,
-                     n, NU, unit_first);
-  hipError_t e0 = hipGetLastError();
-  if (e0 != hipSuccess) return e0;
+  if (!have_unit_map) {
+    hipLaunchKernelGGL(dev::crc32c_unit_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, lc.stream, chunk_start,
+                       n, NU, unit_first);
+    hipError_t e0 = hipGetLastError();
+    if (e0 != hipSuccess) return e0;
+  }
   dev::VarGeom g{base, offsets, lengths, chunk_start, unit_first, n, init, init_all};
   dev::KArgs ka{out, flags, recs, lc.tables};
   hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0, lc.stream, g, ka);

@@ -231,3 +231,59 @@ def ref(flavour: str = "sse") -> _Ref:
 
 def ref_available(flavour: str = "sse") -> bool:
     return os.path.exists(os.path.join(HERE, "_ref", f"libref_crc32c_{flavour}.so"))
+
+
+class _RefFraming:
+    """ctypes view of ``oracle/_ref/libref_framing.so`` (oracle/ref_framing.cc):
+    the reference's own log::Writer, log::Reader and ReadBlock."""
+
+    def __init__(self) -> None:
+        self.path = os.path.join(HERE, "_ref", "libref_framing.so")
+        lib = ctypes.CDLL(self.path, mode=os.RTLD_LOCAL)
+        vp, u64, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t
+        lib.ref_log_write.restype = ctypes.c_int
+        lib.ref_log_write.argtypes = [vp, vp, sz, u64, vp, sz, vp]
+        lib.ref_log_read.restype = ctypes.c_int
+        lib.ref_log_read.argtypes = [vp, sz, ctypes.c_int, u64, vp, sz, vp]
+        lib.ref_read_block.restype = ctypes.c_int
+        lib.ref_read_block.argtypes = [vp, sz, u64, u64, ctypes.c_char_p, sz]
+        self.lib = lib
+
+    def log_write(self, payloads: list[bytes], dest_length: int = 0) -> bytes:
+        blob = b"".join(payloads) or b"\0"
+        lens = np.array([len(p) for p in payloads] or [0], dtype=np.uint64)
+        total = sum(len(p) for p in payloads)
+        cap = total + 7 * (total // 8 + len(payloads) + 2) + 64
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        rc = self.lib.ref_log_write(blob, lens.ctypes.data, len(payloads), dest_length, out, cap, ctypes.byref(n))
+        assert rc == 0, rc
+        return out.raw[:n.value]
+
+    def log_read(self, image: bytes, checksum: bool = True, initial_offset: int = 0) -> str:
+        cap = 64 * (len(image) // 7 + 16) + 4096
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        rc = self.lib.ref_log_read(image or b"\0", len(image), int(checksum), initial_offset, out, cap,
+                                   ctypes.byref(n))
+        assert rc == 0, rc
+        return out.raw[:n.value].decode()
+
+    def read_block(self, image: bytes, offset: int, size: int) -> str:
+        msg = ctypes.create_string_buffer(256)
+        self.lib.ref_read_block(image or b"\0", len(image), offset, size, msg, 256)
+        return msg.value.decode()
+
+
+_ref_framing = None
+
+
+def ref_framing() -> _RefFraming:
+    global _ref_framing
+    if _ref_framing is None:
+        _ref_framing = _RefFraming()
+    return _ref_framing
+
+
+def ref_framing_available() -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libref_framing.so"))

@@ -138,6 +138,34 @@ def framing() -> dict:
     return {"sstable_blocks": blocks, "log_records": records}
 
 
+def log_cases() -> dict:
+    """Log scenarios (tests/framing_cases.py) run through the REFERENCE's own
+    log::Writer (db/log_writer.cc) and log::Reader (db/log_reader.cc), built
+    from /root/reference into oracle/_ref/libref_framing.so."""
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN)))
+    import framing_cases as fc  # tests/framing_cases.py
+    p = oracle.port()
+    rf = oracle.ref_framing()
+    cases = []
+    for spec in fc.named() + fc.random_cases(300):
+        img = fc.write_image(p, spec, rf.log_write)
+        muts, io = fc.resolve(p, spec, img)
+        bad = fc.mutate(p, img, muts)
+        trace = rf.log_read(bad, spec["checksum"], io)
+        c = dict(spec)
+        c.update({"image_len": len(img), "image_crc": p.value(img), "mutations": muts,
+                  "initial_offset": io, "read_len": len(bad), "read_crc": p.value(bad)})
+        c.pop("mutations_rel", None)
+        c.pop("initial_offset_rel", None)
+        if len(trace) <= 6000:
+            c["trace"] = trace
+        else:
+            c["trace_crc"] = p.value(trace.encode())
+            c["trace_lines"] = trace.count("\n")
+        cases.append(c)
+    return {"cases": cases}
+
+
 def configs(do_cfg4: bool) -> dict:
     p = oracle.port()
     r = oracle.ref("sse")
@@ -181,16 +209,23 @@ def configs(do_cfg4: bool) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-cfg4", action="store_true")
+    ap.add_argument("--only", default="", help="comma list of fixtures to regenerate (kat,sweep,framing,log_cases,configs)")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
     os.makedirs(GOLDEN, exist_ok=True)
     provenance = {"generator": "oracle/gen_golden.py",
-                  "reference_builds": [oracle.ref("sse").path, oracle.ref("table").path]}
-    for name, fn in [("kat", kat), ("sweep", sweep), ("framing", framing)]:
+                  "reference_builds": [oracle.ref("sse").path, oracle.ref("table").path,
+                                       os.path.join(os.path.dirname(oracle.ref("sse").path), "libref_framing.so")]}
+    for name, fn in [("kat", kat), ("sweep", sweep), ("framing", framing), ("log_cases", log_cases)]:
+        if only and name not in only:
+            continue
         d = fn()
         d["provenance"] = provenance
         with open(os.path.join(GOLDEN, f"{name}.json"), "w") as f:
             json.dump(d, f, separators=(",", ":"))
         print("wrote", name)
+    if only and "configs" not in only:
+        return
     d = configs(not args.no_cfg4)
     d["provenance"] = provenance
     with open(os.path.join(GOLDEN, "configs.json"), "w") as f:

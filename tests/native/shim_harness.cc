@@ -1,0 +1,77 @@
+// tests/native/shim_harness.cc -- extern "C" driver of the header-only shims
+// (include/nvl_leveldb_shims.h) for tests/test_framing.py: the same call
+// sequence and trace format as oracle/ref_framing.cc drives the reference's
+// log::Writer / log::Reader with, so the two traces compare line for line.
+// This is the binding a LevelDB test would add; it is test code, not product.
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "nvl_leveldb_shims.h"
+
+namespace {
+
+struct TraceReporter : nvl::shims::LogReader::Reporter {
+  std::string* trace;
+  void Corruption(size_t bytes, const char* reason) override {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "C %zu Corruption: ", bytes);
+    trace->append(buf);
+    trace->append(reason);
+    trace->push_back('\n');
+  }
+};
+
+int copy_out(const std::string& s, void* out, size_t cap, size_t* out_len) {
+  *out_len = s.size();
+  if (s.size() > cap) return NVL_CRC32C_ENOSPC;
+  memcpy(out, s.data(), s.size());
+  return NVL_CRC32C_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// nvl::shims::LogWriter over n records (payloads concatenated), appending to a
+// file of dest_length bytes; the sealed new bytes go to out.
+__attribute__((visibility("default")))
+int shim_log_write(const uint8_t* payloads, const uint64_t* lens, size_t n, uint64_t dest_length, uint32_t flags,
+                   uint8_t* out, size_t cap, size_t* out_len) {
+  nvl::shims::LogWriter w(dest_length);
+  const char* p = reinterpret_cast<const char*>(payloads);
+  for (size_t i = 0; i < n; ++i) {
+    w.AddRecord(p, lens[i]);
+    p += lens[i];
+  }
+  std::string img;
+  const int rc = w.Take(&img, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+  return copy_out(img, out, cap, out_len);
+}
+
+// nvl::shims::LogReader over a log image; trace format of ref_log_read.
+__attribute__((visibility("default")))
+int shim_log_read(const uint8_t* file, size_t len, int checksum, uint64_t initial_offset, uint32_t flags,
+                  char* trace, size_t cap, size_t* trace_len) {
+  std::string t;
+  TraceReporter rep;
+  rep.trace = &t;
+  nvl::shims::LogReader r(reinterpret_cast<const char*>(file), len, &rep, checksum != 0, initial_offset, flags);
+  const char* d;
+  size_t n;
+  std::string scratch;
+  while (r.ReadRecord(&d, &n, &scratch)) {
+    char buf[96];
+    snprintf(buf, sizeof(buf), "R %llu %zu %u\n", (unsigned long long)r.LastRecordOffset(), n,
+             nvl_crc32c_value(d, n));
+    t.append(buf);
+  }
+  if (r.status() != NVL_CRC32C_OK) return r.status();
+  t.append("E\n");
+  return copy_out(t, trace, cap, trace_len);
+}
+
+}  // extern "C"

@@ -38,7 +38,8 @@ def test_abi_version_and_strerror(L):
 
 def test_header_compiles_as_c_and_cpp(tmp_path):
     src = tmp_path / "t.c"
-    src.write_text('#include "nvl_crc32c.h"\nint main(void){return nvl_crc32c_abi_version()==NVL_CRC32C_ABI_VERSION?0:1;}\n')
+    src.write_text('#include "nvl_crc32c.h"\n#include "nvl_framing.h"\n'
+                   'int main(void){return nvl_crc32c_abi_version()==NVL_CRC32C_ABI_VERSION?0:1;}\n')
     inc = os.path.join(ROOT, "include")
     lib = os.path.join(ROOT, "nvlevelz_amd")
     for cc, ext in (("gcc", "c"), ("g++", "cc")):

@@ -1,0 +1,258 @@
+"""The §8f call-site shims (include/nvl_framing.h, include/nvl_leveldb_shims.h):
+log::Writer / log::Reader and SSTable block trailers with their CRCs batched.
+
+Parity anchors:
+* tests/golden/log_cases.json -- scenarios after db/log_test.cc plus seeded
+  random ones (tests/framing_cases.py), each written and read by the
+  REFERENCE's own db/log_writer.cc and db/log_reader.cc (oracle/ref_framing.cc,
+  built from /root/reference): the image bytes (crc + length) and the full
+  reader trace -- records returned, LastRecordOffset, every corruption report
+  with its byte count and reason.
+* tests/golden/framing.json -- block trailers / record headers computed with
+  the reference's crc32c.
+* live, where oracle/_ref/libref_framing.so exists: fresh random scenarios
+  against the reference writer/reader, and every sealed or corrupted SSTable
+  block through the reference's ReadBlock (table/format.cc:65-98).
+
+Each check runs twice: NVL_FRAMING_HOST (host CRC; CPU suite) and the GPU
+batch (marked gpu).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import framing_cases as fc
+from conftest import ROOT, gpu_present, load_golden
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+HOST = 0x100
+
+
+@pytest.fixture(scope="module")
+def shim():
+    from nvlevelz_amd import _lib  # noqa: F401  (loads libnvl_crc32c.so first)
+    path = os.path.join(NATIVE, "libshim_harness.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-s", "-C", NATIVE], check=True)
+    lib = ctypes.CDLL(path)
+    vp, u64, sz, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32
+    lib.shim_log_write.restype = ctypes.c_int
+    lib.shim_log_write.argtypes = [vp, vp, sz, u64, u32, vp, sz, vp]
+    lib.shim_log_read.restype = ctypes.c_int
+    lib.shim_log_read.argtypes = [vp, sz, ctypes.c_int, u64, u32, vp, sz, vp]
+    return lib
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nvlevelz_amd import _lib
+    return _lib
+
+
+def _writer(shim, flags):
+    def w(payloads, dest_length):
+        blob = b"".join(payloads) or b"\0"
+        lens = np.array([len(p) for p in payloads] or [0], dtype=np.uint64)
+        total = sum(len(p) for p in payloads)
+        cap = total + 7 * (total // 8 + len(payloads) + 2) + 64
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        rc = shim.shim_log_write(blob, lens.ctypes.data, len(payloads), dest_length, flags, out, cap,
+                                 ctypes.byref(n))
+        assert rc == 0, rc
+        return out.raw[:n.value]
+    return w
+
+
+def _reader(shim, flags):
+    def r(image, checksum, initial_offset):
+        cap = 64 * (len(image) // 7 + 16) + 4096
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        rc = shim.shim_log_read(image or b"\0", len(image), int(checksum), initial_offset, flags, out, cap,
+                                ctypes.byref(n))
+        assert rc == 0, rc
+        return out.raw[:n.value].decode()
+    return r
+
+
+def _check_log_fixtures(shim, port, flags):
+    cases = load_golden("log_cases")["cases"]
+    assert len(cases) >= 300
+    w, r = _writer(shim, flags), _reader(shim, flags)
+    for c in cases:
+        img = fc.write_image(port, c, w)
+        assert (len(img), port.value(img)) == (c["image_len"], c["image_crc"]), c["name"]
+        bad = fc.mutate(port, img, c["mutations"])
+        assert (len(bad), port.value(bad)) == (c["read_len"], c["read_crc"]), c["name"]
+        trace = r(bad, c["checksum"], c["initial_offset"])
+        if "trace" in c:
+            assert trace == c["trace"], c["name"]
+        else:
+            assert (port.value(trace.encode()), trace.count("\n")) == (c["trace_crc"], c["trace_lines"]), c["name"]
+
+
+def test_log_fixtures_host(shim, port):
+    _check_log_fixtures(shim, port, HOST)
+
+
+@pytest.mark.gpu
+def test_log_fixtures_gpu(shim, port):
+    if not gpu_present():
+        pytest.skip("no GPU")
+    _check_log_fixtures(shim, port, 0)
+
+
+def test_log_vs_reference_live(shim, port):
+    import oracle
+    if not oracle.ref_framing_available():
+        pytest.skip("reference framing harness not built")
+    rf = oracle.ref_framing()
+    w, r = _writer(shim, HOST), _reader(shim, HOST)
+    for spec in fc.random_cases(150, seed=777):
+        ref_img = fc.write_image(port, spec, rf.log_write)
+        assert fc.write_image(port, spec, w) == ref_img, spec["name"]
+        muts, io = fc.resolve(port, spec, ref_img)
+        bad = fc.mutate(port, ref_img, muts)
+        assert r(bad, spec["checksum"], io) == rf.log_read(bad, spec["checksum"], io), spec["name"]
+
+
+def test_log_scan_arguments(L):
+    ev = (L.LogEvent * 4)()
+    n = ctypes.c_size_t(0)
+    assert L.lib.nvl_log_scan(None, 0, 5, 1, ev, 4, ctypes.byref(n), HOST) == L.EINVAL  # start not block-aligned
+    assert L.lib.nvl_log_scan(None, 0, 0, 1, ev, 4, None, HOST) == L.EINVAL
+    assert L.lib.nvl_log_scan(None, 0, 0, 1, ev, 4, ctypes.byref(n), HOST) == L.OK
+    assert n.value == 1 and ev[0].kind == L.LOG_EOF
+    img = bytes(7) + b"abc"  # a zero record, then garbage
+    assert L.lib.nvl_log_scan(img, len(img), 0, 1, None, 0, ctypes.byref(n), HOST) == L.OK and n.value == 2  # ZERO, EOF
+    assert L.lib.nvl_log_scan(img, len(img), 0, 1, ev, 1, ctypes.byref(n), HOST) == L.ENOSPC
+
+
+def test_log_record_headers_golden(L, port):
+    """framing.json log records: header CRC of type | payload, via nvl_log_seal."""
+    for rec in load_golden("framing")["log_records"]:
+        payload = port.fill(int(rec["seed"]), 0, int(rec["len"])).tobytes()
+        n = len(payload)
+        img = bytearray(b"\0\0\0\0" + bytes([n & 0xFF, n >> 8, int(rec["type"])]) + payload)
+        off = np.array([0], dtype=np.uint64)
+        assert L.lib.nvl_log_seal((ctypes.c_char * len(img)).from_buffer(img), len(img), off.ctypes.data, 1,
+                                  HOST) == 0
+        assert int.from_bytes(img[:4], "little") == int(rec["masked"])
+
+
+# ---------------------------------------------------------------- SSTable --
+
+def _table(port, seed, nblocks):
+    """A table-file-like image: blocks of random size and type, 5-byte trailers
+    (type, zero CRC), random filler between some of them (index/footer bytes)."""
+    rng = np.random.default_rng(seed)
+    img = bytearray()
+    handles = []
+    for i in range(nblocks):
+        if rng.random() < 0.2:
+            img += port.fill(seed * 1000 + i, 7, int(rng.integers(1, 64))).tobytes()
+        n = int(rng.choice([0, 1, 3, 4, 5, 17, 64, 4096, 4100, int(rng.integers(0, 9000))]))
+        handles.append((len(img), n))
+        img += port.fill(seed * 1000 + i, 0, n).tobytes()
+        img += bytes([int(rng.choice([0, 0, 0, 1]))]) + bytes(4)
+    return img, np.array(handles, dtype=np.uint64).reshape(-1, 2)
+
+
+def _seal(L, img, handles, flags):
+    buf = (ctypes.c_char * len(img)).from_buffer(img)
+    h = np.ascontiguousarray(handles, dtype=np.uint64)
+    return L.lib.nvl_sstable_seal_trailers(buf, len(img), h.ctypes.data, len(h), flags)
+
+
+def _verify(L, img, handles, flags):
+    h = np.ascontiguousarray(handles, dtype=np.uint64)
+    v = np.zeros(len(h), dtype=np.uint8)
+    nb = ctypes.c_uint64(0)
+    rc = L.lib.nvl_sstable_verify_blocks(bytes(img), len(img), h.ctypes.data, len(h), v.ctypes.data,
+                                         ctypes.byref(nb), flags)
+    assert rc == 0, rc
+    assert nb.value == int((v != 0).sum())
+    return v
+
+
+def _ref_verdict(msg, block_type):
+    """ReadBlock's Status text -> NVL_BLOCK_* (type 1 blocks are then decompressed
+    by ReadBlock; without snappy that fails, and it is out of the shim's scope)."""
+    if msg == "" or (block_type == 1 and msg == "Corruption: corrupted compressed block contents"):
+        return 0
+    return {"Corruption: truncated block read": 1, "Corruption: block checksum mismatch": 2,
+            "Corruption: bad block type": 3}[msg]
+
+
+def _check_sstable(L, port, flags):
+    import oracle
+    rf = oracle.ref_framing() if oracle.ref_framing_available() else None
+    for seed in range(1, 9):
+        img, hs = _table(port, seed, 60)
+        assert _seal(L, img, hs, flags) == 0
+        for off, n in hs:  # table_builder.cc:185-187
+            off, n = int(off), int(n)
+            want = port.mask(port.value(bytes(img[off:off + n + 1])))
+            assert int.from_bytes(img[off + n + 1:off + n + 5], "little") == want
+        assert not _verify(L, img, hs, flags).any()
+        rng = np.random.default_rng(seed)
+        bad = bytearray(img)
+        for _ in range(12):  # corrupt contents, type bytes, stored CRCs
+            k = int(rng.integers(0, len(hs)))
+            off, n = int(hs[k][0]), int(hs[k][1])
+            what = rng.integers(0, 3)
+            if what == 0 and n:
+                bad[off + int(rng.integers(0, n))] ^= 1 << int(rng.integers(0, 8))
+            elif what == 1:
+                bad[off + n] = int(rng.integers(2, 256))
+                bad[off + n + 1:off + n + 5] = int(port.mask(port.value(bytes(bad[off:off + n + 1])))).to_bytes(
+                    4, "little")
+            else:
+                bad[off + n + 1 + int(rng.integers(0, 4))] ^= 0x40
+        hs2 = np.concatenate([hs, np.array([[len(bad) - 3, 0], [len(bad) + 10, 5]], dtype=np.uint64)])
+        v = _verify(L, bad, hs2, flags)
+        assert v[-2] == 1 and v[-1] == 1  # truncated
+        for k in range(len(hs)):
+            off, n = int(hs[k][0]), int(hs[k][1])
+            crc_ok = port.value(bytes(bad[off:off + n + 1])) == port.unmask(
+                int.from_bytes(bad[off + n + 1:off + n + 5], "little"))
+            want = 2 if not crc_ok else (3 if bad[off + n] > 1 else 0)
+            assert v[k] == want, (seed, k)
+            if rf is not None:
+                assert _ref_verdict(rf.read_block(bytes(bad), off, n), bad[off + n]) == want, (seed, k)
+
+
+def test_sstable_seal_verify_host(L, port):
+    _check_sstable(L, port, HOST)
+
+
+@pytest.mark.gpu
+def test_sstable_seal_verify_gpu(L, port):
+    if not gpu_present():
+        pytest.skip("no GPU")
+    _check_sstable(L, port, 0)
+
+
+def test_sstable_trailers_golden(L):
+    """framing.json SSTable blocks: trailer = Mask(Value(block | type)) from the reference."""
+    for b in load_golden("framing")["sstable_blocks"]:
+        data = bytes.fromhex(b["hex"])
+        img = bytearray(data + bytes([int(b["type"])]) + bytes(4))
+        assert _seal(L, img, np.array([[0, len(data)]], dtype=np.uint64), HOST) == 0
+        assert int.from_bytes(img[-4:], "little") == int(b["masked"])
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
+def test_device_mode_fails_loudly_without_gpu(L):
+    img = bytearray(b"abc" + bytes(5))
+    h = np.array([[0, 3]], dtype=np.uint64)
+    assert _seal(L, img, h, 0) in (L.ENODEV, L.EHIP)
+    assert img[-4:] == bytes(4)  # nothing written
+    n = ctypes.c_size_t(0)
+    log = bytes(7)
+    log = b"\x01\x02\x03\x04\x01\x00\x01x"
+    assert L.lib.nvl_log_scan(log, len(log), 0, 1, None, 0, ctypes.byref(n), 0) in (L.ENODEV, L.EHIP)

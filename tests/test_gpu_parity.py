@@ -219,6 +219,21 @@ def test_varlen_many_tiny(dev, C, port):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("n", [1, 2, 1023, 1025, 32767, 32768, 32769, 150_000])
+def test_varlen_plan_paths(dev, C, port, n):
+    """Both variable-length plans -- one-workgroup (n <= 32768) and counts ->
+    device scan -> unit map (larger n) -- around the switch-over point."""
+    rng = np.random.default_rng(n)
+    lens = np.where(rng.random(n) < 0.9, rng.integers(0, 600, n), rng.integers(0, 30000, n)).astype(np.int64)
+    offs = (np.cumsum(lens + 1) - lens).astype(np.int64)
+    total = int(offs[-1] + lens[-1]) + 64
+    host = port.fill(0x51A + n, 0, total)
+    buf = torch.from_numpy(host).to(dev)
+    got = _varlen(C, dev, buf, offs, lens, init=0x89ABCDEF)
+    want = port.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64), np.full(n, 0x89ABCDEF, dtype=np.uint32))
+    assert np.array_equal(got, want)
+
+
 def test_empty_batches(dev, C):
     buf = torch.zeros(16, dtype=torch.uint8, device=dev)
     assert C.extend_fixed(buf, 0, 0, 0).numel() == 0

@@ -314,10 +314,14 @@ struct VarGeom {
 // length (partial head chunk, realignment, predicated loads: config 3).
 enum LoadMode : int { kAligned = 0, kGeneral = 1 };
 
-// Registers of one chunk as loaded: row j (j = 0..3) is the coalesced 1 KiB
-// wave load of chunk bytes [1024j, 1024j+1024), lane l holding 16 B at 16l; in
-// kGeneral the rows are loaded from the 16-B aligned address below the chunk
-// start and d[16..19] holds the aligned vector just past row 3.
+// Registers of one chunk as loaded.  Load j (j = 0..3) is one coalesced 1 KiB
+// wave load of chunk bytes [1024j, 1024j+1024) in a permuted lane order: lane
+// (a, b) = (lane >> 4, lane & 15) takes the 16 B at 1024j + 64b + 16a, so that
+// the 4x4 exchange across 16-lane rows in row_transpose leaves lane P holding
+// the 64 contiguous bytes [64P, 64P+64) -- piece P = lane.  In kGeneral the
+// loads start at the aligned address below the chunk start (16-B for a head
+// chunk, 4-B for a body chunk) and d[16..19] holds the bytes just past the
+// last piece (wave-uniform, scalar loaded).
 struct Chunk {
   uint32_t d[20];
 };
@@ -326,9 +330,15 @@ __device__ __forceinline__ uintptr_t chunk_end(const BufInfo& bi, uint32_t c) {
   return (uintptr_t)bi.p + bi.len - (uint64_t)kChunk * (bi.J - 1u - c);
 }
 
+// Byte offset of the lane's 16 B within each 1 KiB load.
+__device__ __forceinline__ uint32_t lane_load_off(int lane) {
+  return ((uint32_t)(lane & 15) << 6) | ((uint32_t)(lane >> 4) << 4);
+}
+
 template <int M>
 __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int lane, Chunk& ch) {
   const uintptr_t ce = chunk_end(bi, c);
+  const uint32_t lo = lane_load_off(lane);
   if constexpr (M == kAligned) {
 #if defined(NVL_ABL_NOLOAD)  // ablation: synthetic data, no global loads
 #pragma unroll
@@ -337,7 +347,7 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
 #endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const u32x4 v = ld16(ce - kChunk + 1024u * (uint32_t)j + 16u * (uint32_t)lane);
+      const u32x4 v = ld16(ce - kChunk + 1024u * (uint32_t)j + lo);
       ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
     }
   } else {
@@ -346,13 +356,13 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
     if (ce - kChunk < p + 4) {
       // Head chunk: 16-B aligned loads below the chunk start (never crossing
       // into a page the buffer does not touch), vectors wholly before the
-      // buffer skipped; the aligned vector just past row 3 is the same for
-      // every lane: a scalar load (SGPRs) ending inside ce's 16-B granule.
+      // buffer skipped; the aligned vector just past the last piece is the
+      // same for every lane: a scalar load (SGPRs) ending inside ce's granule.
       const uint32_t m = (uint32_t)(ce & 15u);
       const uintptr_t A = ce - kChunk - m;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uintptr_t addr = A + 1024u * (uint32_t)j + 16u * (uint32_t)lane;
+        const uintptr_t addr = A + 1024u * (uint32_t)j + lo;
         u32x4 v = {0u, 0u, 0u, 0u};
         if (addr + 16u > p) v = ld16(addr);
         ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
@@ -362,15 +372,15 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
       ch.d[16] = x.x; ch.d[17] = x.y; ch.d[18] = x.z; ch.d[19] = x.w;
     } else {
       // Body chunk: every byte of [ce-4096-3, ce) lies inside the buffer, so
-      // the rows are loaded at the DWORD-aligned address below the chunk
-      // start (gfx950 serves 4-B aligned dwordx4 at full rate, byte-misaligned
-      // at ~80 %: tools/diag/unaligned.hip); the dword past row 3 (scalar)
-      // completes lane 63.
+      // the loads start at the DWORD-aligned address below the chunk start
+      // (gfx950 serves 4-B aligned dwordx4 at full rate, byte-misaligned at
+      // ~80 %: tools/diag/unaligned.hip); the dword past the last piece
+      // (scalar) completes lane 63.
       const uint32_t r = (uint32_t)(ce & 3u);
       const uintptr_t A4 = ce - kChunk - r;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + 16u * (uint32_t)lane);
+        const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
         ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
       }
       ch.d[16] = r ? *reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(A4 + kChunk) : 0u;
@@ -379,51 +389,61 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
   }
 }
 
-// 4x4 transpose of 16-byte slots inside each lane quad (DPP quad_perm):
-// afterwards lane 4q+r holds, in slot s, what lane 4q+s held in slot r.
-__device__ __forceinline__ void quad_transpose(int lane, uint32_t (&d)[16]) {
-  const int r = lane & 3;
-  const bool t1[4] = {(r >> 1) != 0, (r >> 1) != 0, (r >> 1) == 0, (r >> 1) == 0};  // bit1(j) != bit1(r)
-  const bool t0[4] = {(r & 1) != 0, (r & 1) == 0, (r & 1) != 0, (r & 1) == 0};      // bit0(j) != bit0(r)
+// 4x4 transpose of 16-byte slots across the four 16-lane rows: slot j of lane
+// (a, b) <- slot a of lane (j, b).  Two v_permlane32_swap + two
+// v_permlane16_swap per dword column (16 VALU per chunk), no temporaries.
+__device__ __forceinline__ void row_transpose(uint32_t (&d)[16]) {
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {  // one dword column at a time: 4 live temporaries
-    uint32_t a[4], b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = d[4 * j + x];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // stage 1: swap 2x2 blocks across lane bit 1
-      const uint32_t o = dpp_xor2(a[j ^ 2]);
-      b[j] = t1[j] ? o : a[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // stage 2: swap within 2x2 blocks across lane bit 0
-      const uint32_t o = dpp_xor1(b[j ^ 1]);
-      d[4 * j + x] = t0[j] ? o : b[j];
-    }
+  for (int x = 0; x < 4; ++x) {
+    const auto r02 = __builtin_amdgcn_permlane32_swap(d[x], d[8 + x], false, false);
+    const auto r13 = __builtin_amdgcn_permlane32_swap(d[4 + x], d[12 + x], false, false);
+    const auto q01 = __builtin_amdgcn_permlane16_swap(r02[0], r13[0], false, false);
+    const auto q23 = __builtin_amdgcn_permlane16_swap(r02[1], r13[1], false, false);
+    d[x] = q01[0];
+    d[4 + x] = q01[1];
+    d[8 + x] = q23[0];
+    d[12 + x] = q23[1];
   }
 }
 
-// The lane's 16 words, transposed so lane 4q+r holds chunk piece P = 16r + q
-// (64 contiguous bytes), with the ~init injection and, on the head chunk, the
-// zero-masking of bytes before the buffer start.
+// Next lane's dword (DPP wave_shl:1); lane 63 gets `last`.
+__device__ __forceinline__ uint32_t next_lane(uint32_t v, uint32_t last) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+// Head-chunk realign for a dword shift Q (compile-time) and byte shift r:
+// out[k] = bytes [4(k+Q) + r, +4) of the lane's piece extended by nx[].
+template <int Q>
+__device__ __forceinline__ void realign_q(uint32_t (&w)[16], const uint32_t (&nx)[4], uint32_t r) {
+  uint32_t e[20];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) e[k] = w[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[16 + k] = nx[k];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(e[k + Q + 1], e[k + Q], r);
+}
+
+// The lane's 16 words of piece P = lane (64 contiguous bytes), with the ~init
+// injection and, on the head chunk, the zero-masking of bytes before the
+// buffer start.
 template <int M>
 __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int lane, const Chunk& ch,
                                             uint32_t (&w)[16]) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
-  if constexpr (M == kAligned) {
 #if !defined(NVL_ABL_NOLOAD)
-    quad_transpose(lane, w);
+  row_transpose(w);
 #endif
-    if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0
+  if constexpr (M == kAligned) {
+    if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0, word 0
   } else {
     const uintptr_t ce = chunk_end(bi, c);
     const bool head = ce - kChunk < (uintptr_t)bi.p + 4;
-    // Shift the loaded rows left by sh bytes: head chunks were loaded from the
-    // 16-B aligned address below the chunk start (sh = ce & 15), body chunks
-    // from the 4-B aligned one (sh = ce & 3).  Lane l's bytes continue in lane
-    // l+1 (DPP wave_shl:1); lane 63 continues in lane 0 of the next row
-    // (wave_rol:1) or, after row 3, in the scalar extra.
+    // Shift the pieces left by sh bytes: head chunks were loaded from the 16-B
+    // aligned address below the chunk start (sh = ce & 15), body chunks from
+    // the 4-B aligned one (sh = ce & 3).  Lane P's bytes continue in lane P+1
+    // and, for lane 63, in the scalar extra.
     const uint32_t sh = head ? (uint32_t)(ce & 15u) : (uint32_t)(ce & 3u);
 #if defined(NVL_ABL_NOREALIGN)
     if (false) {
@@ -431,43 +451,23 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
     if (sh != 0) {
 #endif
       const uint32_t r = sh & 3u;
-      if (sh >= 4) {  // head chunk with a dword shift: all four next-lane dwords
+      if (head) {
+        uint32_t nx[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t e[8];
-#pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            const uint32_t old = j < 3 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)ch.d[4 * (j + 1) + x], 0x134, 0xF, 0xF, true)
-                                       : ch.d[16 + x];
-            e[x] = ch.d[4 * j + x];
-            e[4 + x] = (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)ch.d[4 * j + x], 0x130, 0xF, 0xF, false);
-          }
-          // dword shift sh>>2 as two levels of v_perm_b32 whose selector picks
-          // a whole source dword (a plain select here becomes a scratch-indexed
-          // load), then v_alignbyte_b32 for the byte shift sh&3.
-          const uint32_t s1 = (sh & 8u) ? 0x07060504u : 0x03020100u;
-          const uint32_t s0 = (sh & 4u) ? 0x07060504u : 0x03020100u;
-          uint32_t f[6], gg[5];
-#pragma unroll
-          for (int k = 0; k < 6; ++k) f[k] = __builtin_amdgcn_perm(e[k + 2], e[k], s1);
-#pragma unroll
-          for (int k = 0; k < 5; ++k) gg[k] = __builtin_amdgcn_perm(f[k + 1], f[k], s0);
-#pragma unroll
-          for (int x = 0; x < 4; ++x) w[4 * j + x] = __builtin_amdgcn_alignbyte(gg[x + 1], gg[x], r);
+        for (int k = 0; k < 4; ++k) nx[k] = next_lane(w[k], ch.d[16 + k]);
+        switch (sh >> 2) {  // wave-uniform: one straight-line variant per dword shift
+          case 0: realign_q<0>(w, nx, r); break;
+          case 1: realign_q<1>(w, nx, r); break;
+          case 2: realign_q<2>(w, nx, r); break;
+          default: realign_q<3>(w, nx, r); break;
         }
-      } else {  // byte shift only: one next-lane dword per row
+      } else {
+        const uint32_t nx = next_lane(w[0], ch.d[16]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t old = j < 3 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)ch.d[4 * (j + 1)], 0x134, 0xF, 0xF, true)
-                                     : ch.d[16];
-          const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)ch.d[4 * j], 0x130, 0xF, 0xF, false);
-#pragma unroll
-          for (int x = 0; x < 4; ++x)
-            w[4 * j + x] = __builtin_amdgcn_alignbyte(x < 3 ? ch.d[4 * j + x + 1] : nx, ch.d[4 * j + x], r);
-        }
+        for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+        w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
       }
     }
-    quad_transpose(lane, w);
     const uintptr_t p = (uintptr_t)bi.p;
 #if defined(NVL_ABL_NOMASK)
     if (false) {
@@ -475,20 +475,19 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
     if (head) {  // chunk holds the buffer head (or the tail of its ~init)
 #endif
       // d0 = buffer start - chunk start, in (-4, 4096) for a head chunk;
-      // rel = bytes of this lane's piece (P = 16*(lane&3) + (lane>>2)) before
-      // the buffer start.  Word k keeps its bytes at or after the start and
-      // takes the ~init bytes at [rel, rel+4): both from 64-bit shifts whose
-      // clamped amounts make the out-of-range cases come out as 0 / all-ones.
+      // rel = bytes of this lane's piece (P = lane) before the buffer start.
+      // Word k keeps its bytes at or after the start and takes the ~init
+      // bytes at [rel, rel+4): both from 64-bit shifts whose clamped amounts
+      // make the out-of-range cases come out as 0 / all-ones.
       const int d0 = (int)(int64_t)(p - (ce - kChunk));
-      const uint32_t l = opaque((uint32_t)lane);
-      const int P = (int)(((l & 3u) << 4) | (l >> 2));
+      const int P = (int)opaque((uint32_t)lane);
       const int rel = min(max(d0 - 64 * P, -8), 72);
       const uint64_t s_hi = (uint64_t)bi.s << 32;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int sh = rel - 4 * k;
-        const uint32_t keep = (uint32_t)(~0ull << (8 * min(max(sh, 0), 4)));
-        const uint32_t inj = (uint32_t)(s_hi >> ((32 - 8 * min(max(sh, -4), 4)) & 63));
+        const int shk = rel - 4 * k;
+        const uint32_t keep = (uint32_t)(~0ull << (8 * min(max(shk, 0), 4)));
+        const uint32_t inj = (uint32_t)(s_hi >> ((32 - 8 * min(max(shk, -4), 4)) & 63));
         w[k] = (w[k] & keep) ^ inj;
       }
     }
@@ -518,20 +517,21 @@ __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, c
 #pragma unroll
     for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
   }
-  // Lane -> stream position P = 16*(lane&3) + (lane>>2): lane bits 0,1 step
-  // 1024/2048 bytes (comb tables 4, 5), bits 2..5 step 64..512 (tables 0..3).
+  // Lane = stream position P: lane bit k steps 64*2^k bytes (comb table k).
+  // Bits 0 and 1 go first: afterwards the lanes of a quad hold equal values,
+  // which fold_level's quad-spread byte lookups rely on.
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, 4>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<0>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, 5>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<1>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, 0>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<2>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, 1>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<3>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, 2>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<4>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, 3>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<5>(lds, crc[u], lane);
 #pragma unroll
   for (int u = 0; u < U; ++u) raw[u] = crc[u];
 }
@@ -949,60 +949,77 @@ __device__ __forceinline__ uint64_t ceil_div_u64(uint64_t a, uint64_t d) {
 // The whole variable-length plan in one workgroup, for batches of up to
 // kPlanSmallMax buffers: chunk counts, their exclusive prefix (chunk_start,
 // cs[n] = T) and the unit map -- one launch instead of counts + device scan +
-// unit map.  The chunk counts are staged in LDS by one fully parallel,
-// coalesced pass; the prefix is then scanned tile by tile (1024 buffers, thread
-// t holding buffer 1024k + t) out of LDS.
+// unit map.  The chunk counts are staged in LDS by one coalesced pass; thread
+// t then owns the contiguous buffer run [t*per, t*per + per): one block-wide
+// scan of the run sums, and each thread walks its run in registers.
 constexpr uint64_t kPlanThreads = 1024;
 constexpr uint64_t kPlanSmallMax = 32768;
+
+__device__ __forceinline__ uint32_t plan_pad(uint32_t i) { return i + (i >> 5); }  // 33 words per 32: no bank conflicts
 
 __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t* __restrict__ lengths, uint64_t n,
                                                                 uint64_t NU, uint64_t* __restrict__ cs,
                                                                 uint64_t* __restrict__ unit_first) {
-  __shared__ uint32_t js[kPlanSmallMax];  // chunk counts (a buffer of < 2^40 bytes has < 2^28 chunks)
+  __shared__ uint32_t js[kPlanSmallMax + kPlanSmallMax / 32];  // chunk counts, then run-relative prefixes
   __shared__ uint64_t wsum[kPlanThreads / kWave];
+  __shared__ uint64_t rstart[kPlanThreads];  // first chunk of each thread's run
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t nn = (uint32_t)n;
-#pragma unroll 8
-  for (uint32_t i = t; i < nn; i += kPlanThreads) {
-    const uint64_t L = lengths[i];
-    js[i] = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
+  {  // all of the thread's lengths in flight at once (a loop issues them one latency at a time)
+    constexpr int kPer = (int)(kPlanSmallMax / kPlanThreads);
+    uint64_t Ls[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = t + (uint32_t)k * (uint32_t)kPlanThreads;
+      Ls[k] = i < nn ? lengths[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = t + (uint32_t)k * (uint32_t)kPlanThreads;
+      if (i < nn) js[plan_pad(i)] = Ls[k] <= kChunk ? 1u : (uint32_t)((Ls[k] + kChunk - 1) / kChunk);
+    }
   }
   __syncthreads();
-  uint64_t carry = 0;
-#pragma unroll 1
-  for (uint32_t base = 0; base < nn; base += kPlanThreads) {
-    const uint32_t i = base + t;
-    const uint32_t j = i < nn ? js[i] : 0u;
-    uint64_t x = j;  // inclusive scan over the wave
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(x, o, 64);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint64_t before = 0, tile = 0;
-#pragma unroll
-    for (uint32_t v = 0; v < kPlanThreads / kWave; ++v) {
-      const uint64_t sv = wsum[v];
-      before += v < wv ? sv : 0;
-      tile += sv;
-    }
-    if (i < nn) cs[i] = carry + before + x - j;
-    carry += tile;
-    __syncthreads();  // wsum is reused by the next tile
+  const uint32_t per = (nn + (uint32_t)kPlanThreads - 1) / (uint32_t)kPlanThreads;
+  const uint32_t i0 = min(nn, t * per), i1 = min(nn, i0 + per);
+  // The run's counts become run-relative exclusive prefixes in place (u32: a
+  // device-resident buffer is < 2^38 bytes = 2^26 chunks, a run <= 32 of them).
+  uint32_t sum = 0;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t j = js[plan_pad(i)];
+    js[plan_pad(i)] = sum;
+    sum += j;
   }
-  const uint64_t T = carry;
+  uint64_t x = sum;  // inclusive scan of the run sums over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint64_t before = 0, T = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < kPlanThreads / kWave; ++v) {
+    const uint64_t sv = wsum[v];
+    before += v < wv ? sv : 0;
+    T += sv;
+  }
+  const uint64_t run0 = before + x - sum;
+  rstart[t] = run0;
+  __syncthreads();
+  // chunk_start, coalesced: cs[i] = start of i's run + its run-relative prefix.
+  for (uint32_t i = t; i < nn; i += kPlanThreads) cs[i] = rstart[i / per] + js[plan_pad(i)];
   if (t == 0) cs[n] = T;
-  // Unit map: buffer i owns the units u with cs_i <= floor(T*u/NU) < cs_i + J_i,
-  // i.e. u in [ceil(cs_i*NU/T), ceil((cs_i+J_i)*NU/T)) (see crc32c_unit_map);
-  // cs_i is read back from this thread's own store.
-  for (uint32_t i = t; i < nn; i += kPlanThreads) {
-    const uint64_t c0 = cs[i];
-    const uint64_t u0 = ceil_div_u64(c0 * NU, T);
-    uint64_t u1 = ceil_div_u64((c0 + js[i]) * NU, T);
-    if (u1 > NU) u1 = NU;
-    for (uint64_t u = u0; u < u1; ++u) unit_first[u] = i;
+  // Unit map: unit u starts in buffer i iff cs_i*NU <= T*u < cs_{i+1}*NU
+  // (lo(u) = floor(T*u/NU), see crc32c_unit_map).  Walk the run with the
+  // running products cn = cs_{i+1}*NU and tu = T*u: one division per thread.
+  uint64_t u = ceil_div_u64(run0 * NU, T);
+  uint64_t tu = T * u;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint64_t next = run0 + (i + 1 < i1 ? js[plan_pad(i + 1)] : sum);
+    const uint64_t cn = next * NU;
+    for (; u < NU && tu < cn; ++u, tu += T) unit_first[u] = i;
   }
 }
 

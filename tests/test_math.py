@@ -58,28 +58,35 @@ def test_byte_sliced_operators():
 
 
 def test_fast_path_transposed_fold(port):
-    """Fast path: lane 4q+r holds chunk position 16r+q after the quad
-    transpose; the butterfly over lane bits (0,1,2,3,4,5) must use distances
-    (1024, 2048, 64, 128, 256, 512) bytes."""
+    """Fast path: load j puts bytes [1024j + 64b + 16a, +16) in lane (a, b) =
+    (lane >> 4, lane & 15); the permlane32/permlane16 swap exchange across
+    16-lane rows (row_transpose) leaves lane P holding piece P = bytes
+    [64P, 64P+64); the butterfly over lane bits 0..5 uses distances 64*2^k."""
     data = bytes(port.fill(5, 0, 4096))
-    # the transpose itself: lane l's load j holds bytes [1024j+16l, +16)
+    # M[l][j] = (source lane, load) of the 16 B in lane l, slot j
     M = [[(l, j) for j in range(4)] for l in range(64)]
 
-    def stage(M, m, bit):
-        return [[M[l ^ m][j ^ m] if ((j >> bit) & 1) != (((l & 3) >> bit) & 1) else M[l][j]
-                 for j in range(4)] for l in range(64)]
-    M = stage(stage(M, 2, 1), 1, 0)
+    def swap(M, ra, rb, half):
+        """v_permlane{32,16}_swap on slot registers ra (vdst) and rb (src0):
+        vdst's upper lanes of each 2*half group <-> src0's lower lanes."""
+        out = [row[:] for row in M]
+        for l in range(64):
+            if (l // half) % 2 == 1:          # upper half of vdst swaps with lower half of src0
+                out[l][ra] = M[l - half][rb]
+                out[l - half][rb] = M[l][ra]
+        return out
+    M = swap(swap(M, 0, 2, 32), 1, 3, 32)
+    M = swap(swap(M, 0, 1, 16), 2, 3, 16)
     lanes = []
     for l in range(64):
-        piece = b"".join(data[1024 * j + 16 * src:1024 * j + 16 * src + 16] for (src, j) in M[l])
-        q, r = l >> 2, l & 3
-        assert piece == data[64 * (16 * r + q):64 * (16 * r + q) + 64]
+        src = [(sl >> 4, sl & 15, j) for (sl, j) in M[l]]  # (a, b, load) of each slot
+        piece = b"".join(data[1024 * j + 64 * b + 16 * a:1024 * j + 64 * b + 16 * a + 16] for (a, b, j) in src)
+        assert piece == data[64 * l:64 * l + 64]
         lanes.append(km.raw_bytes(0, piece))
-    ops = [km.COMB[i] for i in (4, 5, 0, 1, 2, 3)]
     g = lanes
     for lev in range(6):
         pt = [g[l ^ (1 << lev)] for l in range(64)]
-        g = [km.apply_op(ops[lev], pt[l] if (l >> lev) & 1 else g[l]) ^ (g[l] if (l >> lev) & 1 else pt[l])
+        g = [km.apply_op(km.COMB[lev], pt[l] if (l >> lev) & 1 else g[l]) ^ (g[l] if (l >> lev) & 1 else pt[l])
              for l in range(64)]
     assert len(set(g)) == 1 and g[0] == km.raw_bytes(0, data)
     assert (~km.raw_bytes(0xFFFFFFFF, data)) & 0xFFFFFFFF == port.value(data)

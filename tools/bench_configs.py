@@ -13,6 +13,8 @@ lib = _lib.lib
 if a.lib:
     lib = ctypes.CDLL(os.path.abspath(a.lib), mode=os.RTLD_LOCAL)
     for name, (res, args) in _lib.SIGNATURES.items():
+        if not hasattr(lib, name):  # older variant builds lack newer entry points
+            continue
         f = getattr(lib, name); f.restype = res; f.argtypes = args
 dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
 assert lib.nvl_crc32c_init(0) == 0

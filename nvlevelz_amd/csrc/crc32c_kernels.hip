@@ -46,11 +46,16 @@ constexpr int kThreads = kWave * kWavesPerWG;  // 1024
 constexpr uint32_t kChunk = 4096;
 
 // LDS image (bytes)
-constexpr uint32_t kRepBytes = 128u * 1024u;           // 4 tables x 256 x 32 replicas x 4 B
-constexpr uint32_t kCombOff = kRepBytes;               // comb[6][4][256] u32
-constexpr uint32_t kShOff = kCombOff + 6u * 4u * 256u * 4u;  // sh4096[4][256] u32
-constexpr uint32_t kCtrOff = kShOff + 4u * 256u * 4u;         // per-workgroup work counter
+// The operator tables sit first so that every table offset of a lookup fits
+// the ds_read 16-bit immediate (comb level k at 4096*k, sh4096 at 24576, the
+// slice image at 28672); only the data-dependent part is computed per lookup.
+constexpr uint32_t kCombOff = 0;                              // comb[6][4][256] u32
+constexpr uint32_t kShOff = kCombOff + 6u * 4u * 256u * 4u;   // sh4096[4][256] u32
+constexpr uint32_t kSliceOff = kShOff + 4u * 256u * 4u;       // 4 tables x 256 x 32 replicas x 4 B
+constexpr uint32_t kRepBytes = 128u * 1024u;
+constexpr uint32_t kCtrOff = kSliceOff + kRepBytes;           // per-workgroup work counter
 constexpr uint32_t kLdsBytes = kCtrOff + 16u;                 // 159760 B
+static_assert(kSliceOff < 65536u && kShOff < 65536u, "table offsets must fit the ds_read immediate");
 static_assert(kLdsBytes <= 160u * 1024u, "LDS image exceeds 160 KiB");
 
 // DevTables word offsets (see crc32c_internal.h)
@@ -129,7 +134,8 @@ __device__ __forceinline__ uint32_t slice4(const uint8_t* lds, uint32_t x, const
   const uint32_t a1 = __builtin_amdgcn_perm(x, lb.t2, 0x0C020500u);
   const uint32_t a2 = __builtin_amdgcn_perm(x, lb.t1, 0x0C020600u);
   const uint32_t a3 = __builtin_amdgcn_perm(x, lb.t0, 0x0C020700u);
-  return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
+  const uint8_t* sl = lds + kSliceOff;
+  return lds_u32(sl, a0) ^ lds_u32(sl, a1) ^ lds_u32(sl, a2) ^ lds_u32(sl, a3);
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -144,15 +150,16 @@ __device__ __forceinline__ uint32_t slice4_x(const uint8_t* lds, uint32_t x, uin
   const uint32_t a1 = __builtin_amdgcn_perm(x, lb.t2, 0x0C020500u);
   const uint32_t a2 = __builtin_amdgcn_perm(x, lb.t1, 0x0C020600u);
   const uint32_t a3 = __builtin_amdgcn_perm(x, lb.t0, 0x0C020700u);
-  return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1), lds_u32(lds, a2)), lds_u32(lds, a3), next);
+  const uint8_t* sl = lds + kSliceOff;
+  return xor3(xor3(lds_u32(sl, a0), lds_u32(sl, a1), lds_u32(sl, a2)), lds_u32(sl, a3), next);
 }
 
 // slice4(x) ^ next -- the chain step with the following word folded in.
 __device__ __forceinline__ uint32_t slice4_next(const uint8_t* lds, uint32_t x, uint32_t next, const LaneBase& lb) {
-#if defined(NVL_XOR3)
-  return slice4_x(lds, x, next, lb);
-#else
+#if defined(NVL_NO_XOR3)
   return slice4(lds, x, lb) ^ next;
+#else
+  return slice4_x(lds, x, next, lb);  // two v_bitop3 instead of four v_xor (tools/ab_bench.py: -2 us on cfg2)
 #endif
 }
 
@@ -167,6 +174,7 @@ __device__ __forceinline__ uint32_t opaque(uint32_t v) {
   return v;
 }
 
+
 // Byte j of v looked up in 1 KiB table (TAB, j): the lane supplies j through
 // (base = table 0's address for its j, sh = 8j); TAB becomes the ds_read
 // immediate offset.
@@ -180,7 +188,7 @@ __device__ __forceinline__ uint32_t lane_lookup(const uint8_t* lds, uint32_t bas
 // group of lower stream positions ("left"), the partner the upper one
 // ("right"); left is shifted by the operator in comb table TAB (64*2^TAB
 // bytes) and XORed in.  Lanes 0..3 of every quad spread the 4 byte lookups.
-template <int LEV, int TAB = LEV>
+template <int LEV, int TAB = LEV, bool OPQ = true>
 __device__ __forceinline__ uint32_t fold_level(const uint8_t* lds, uint32_t g, int lane) {
   const uint32_t pt = lane_xor<LEV>(g);
   const bool hi = (lane >> LEV) & 1;
@@ -188,34 +196,24 @@ __device__ __forceinline__ uint32_t fold_level(const uint8_t* lds, uint32_t g, i
   const uint32_t right = hi ? g : pt;
   uint32_t s;
   if constexpr (LEV == 0) {  // lane bit 0 picks bytes {0,1} or {2,3}
-    const uint32_t h = opaque((uint32_t)lane & 1u);
-    const uint32_t base = kCombOff + (h << 11), sh = h << 4;
-    s = lane_lookup<TAB * 4096u>(lds, base, sh, left) ^ lane_lookup<TAB * 4096u + 1024u>(lds, base, sh + 8u, left);
+    const uint32_t h = OPQ ? opaque((uint32_t)lane & 1u) : (uint32_t)lane & 1u;
+    const uint32_t base = h << 11, sh = h << 4;
+    s = lane_lookup<kCombOff + TAB * 4096u>(lds, base, sh, left) ^
+        lane_lookup<kCombOff + TAB * 4096u + 1024u>(lds, base, sh + 8u, left);
     s ^= dpp_xor1(s);
   } else {  // lane & 3 picks the byte
-    const uint32_t j = opaque((uint32_t)lane & 3u);
-    s = lane_lookup<TAB * 4096u>(lds, kCombOff + (j << 10), j << 3, left);
+    const uint32_t j = OPQ ? opaque((uint32_t)lane & 3u) : (uint32_t)lane & 3u;
+    s = lane_lookup<kCombOff + TAB * 4096u>(lds, j << 10, j << 3, left);
     s ^= dpp_xor1(s);
     s ^= dpp_xor2(s);
   }
   return s ^ right;
 }
 
-// XOR_l shift(g_l, 64*(63-l)) over the wave; every lane gets the result.
-__device__ __forceinline__ uint32_t wave_fold(const uint8_t* lds, uint32_t g, int lane) {
-  g = fold_level<0>(lds, g, lane);
-  g = fold_level<1>(lds, g, lane);
-  g = fold_level<2>(lds, g, lane);
-  g = fold_level<3>(lds, g, lane);
-  g = fold_level<4>(lds, g, lane);
-  g = fold_level<5>(lds, g, lane);
-  return g;
-}
-
 // shift(acc, 4096) for a wave-uniform acc; every lane gets the result.
 __device__ __forceinline__ uint32_t shift4096(const uint8_t* lds, uint32_t acc, int lane) {
   const uint32_t j = opaque((uint32_t)lane & 3u);
-  uint32_t s = lane_lookup<0>(lds, kShOff + (j << 10), j << 3, acc);
+  uint32_t s = lane_lookup<kShOff>(lds, j << 10, j << 3, acc);
   s ^= dpp_xor1(s);
   s ^= dpp_xor2(s);
   return s;
@@ -236,7 +234,7 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restric
     const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
     const uint32_t b = (off >> 8) & 0xFFu;
     const uint32_t v = g[kGSlice + tab * 256u + b];
-    *reinterpret_cast<uint4*>(lds + off) = make_uint4(v, v, v, v);
+    *reinterpret_cast<uint4*>(lds + kSliceOff + off) = make_uint4(v, v, v, v);
   }
   // comb + sh4096 copied verbatim (7168 words = 1792 uint4)
   const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
@@ -343,6 +341,16 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
 #if defined(NVL_ABL_NOLOAD)  // ablation: synthetic data, no global loads
 #pragma unroll
     for (int k = 0; k < 16; ++k) ch.d[k] = (uint32_t)(ce >> 4) * 2654435761u + (uint32_t)(k * 40503 + lane);
+    return;
+#endif
+#if defined(NVL_LD_AUX)  // tuning build: buffer loads with explicit cache-policy bits
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(ce - kChunk), (short)0, (int)kChunk, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(1024u * (uint32_t)j + lo), 0, NVL_LD_AUX);
+      ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+    }
     return;
 #endif
 #pragma unroll
@@ -496,7 +504,9 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
 
 // Serial slice-by-4 chains + butterflies of U chunks from their built words,
 // interleaved so each wave keeps U independent LDS round trips in flight.
-template <int U>
+// OPQ: recompute the per-lane butterfly bases at each use (kGeneral, whose
+// kernels would otherwise spill); the aligned kernels keep them hoisted.
+template <int U, bool OPQ>
 __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16], int lane,
                                        uint32_t (&raw)[U]) {
   uint32_t crc[U];
@@ -517,21 +527,26 @@ __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, c
 #pragma unroll
     for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
   }
+#if defined(NVL_ABL_NOFOLD)  // ablation: chains only, no butterfly
+#pragma unroll
+  for (int u = 0; u < U; ++u) raw[u] = crc[u] ^ dpp_xor1(crc[u]);
+  return;
+#endif
   // Lane = stream position P: lane bit k steps 64*2^k bytes (comb table k).
   // Bits 0 and 1 go first: afterwards the lanes of a quad hold equal values,
   // which fold_level's quad-spread byte lookups rely on.
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<0>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, 0, OPQ>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<1>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, 1, OPQ>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<2>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, 2, OPQ>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<3>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, 3, OPQ>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<4>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, 4, OPQ>(lds, crc[u], lane);
 #pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<5>(lds, crc[u], lane);
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, 5, OPQ>(lds, crc[u], lane);
 #pragma unroll
   for (int u = 0; u < U; ++u) raw[u] = crc[u];
 }
@@ -544,16 +559,17 @@ __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb
   uint32_t w[U][16];
 #pragma unroll
   for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u]);
-  chains<U>(lds, lb, w, lane, raw);
+  chains<U, M == kGeneral>(lds, lb, w, lane, raw);
 }
 
 // Chain + butterfly of one chunk from its built words.
+template <int M>
 __device__ __forceinline__ uint32_t chain_fold(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[16],
                                                int lane) {
   uint32_t w1[1][16], r[1];
 #pragma unroll
   for (int k = 0; k < 16; ++k) w1[0][k] = w[k];
-  chains<1>(lds, lb, w1, lane, r);
+  chains<1, M == kGeneral>(lds, lb, w1, lane, r);
   return r[0];
 }
 
@@ -573,7 +589,7 @@ __device__ __forceinline__ uint32_t tiny_crc(const uint8_t* lds, const BufInfo& 
   uint32_t l = bi.s;  // = ~init
   for (uint32_t k = 0; k < (uint32_t)bi.len; ++k) {
     const uint32_t b = bi.p[k];
-    l = lds_u32(lds, ((l ^ b) & 0xFFu) << 8) ^ (l >> 8);  // T0, replica 0
+    l = lds_u32(lds + kSliceOff, ((l ^ b) & 0xFFu) << 8) ^ (l >> 8);  // T0, replica 0
   }
   return ~l;
 }
@@ -676,6 +692,11 @@ __device__ unsigned long long g_stamps[4 * 65536];
 // of a CU finish together (a static per-wave split left the last wave ~20 %
 // behind the mean: older waves win issue arbitration).  U buffers per unit are
 // computed with interleaved chains.
+#ifndef NVL_TAIL
+#define NVL_TAIL 64  // single-buffer units at the end of a range (tools/ab_bench.py: 64 > 32 > 96 > 16 > 0)
+#endif
+constexpr uint32_t kTail = NVL_TAIL;
+
 template <int U, int NW = kWavesPerWG>
 __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
@@ -683,11 +704,15 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t B0 = g.n * blockIdx.x / gridDim.x;
   const uint64_t B1 = g.n * (blockIdx.x + 1) / gridDim.x;
-  const uint32_t nunits = (uint32_t)((B1 - B0 + U - 1) / U);
+  // The range's last kTail buffers are single-buffer units: a CU's waves
+  // then finish within half a unit of each other instead of a whole one.
+  const uint32_t cnt = (uint32_t)(B1 - B0);
+  const uint32_t nfull = cnt > kTail ? (cnt - kTail) / U : 0u;  // U-buffer units
+  const uint32_t nunits = nfull + (cnt - nfull * U);
 
   auto unit_pos = [&](uint32_t u, int k, Pos& p) -> bool {
-    const uint64_t i = B0 + (uint64_t)u * U + (uint64_t)k;
-    if (u >= nunits || i >= B1) return false;
+    const uint64_t i = u < nfull ? B0 + (uint64_t)u * U + (uint64_t)k : B0 + (uint64_t)nfull * U + (u - nfull);
+    if (u >= nunits || (u >= nfull && k > 0)) return false;
     p.i = i;
     p.c = 0;
     p.bi = g.info(i);
@@ -842,9 +867,9 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
       NVL_COUNT();
       uint32_t r[2];
       if (two) {
-        chains<2>(lds, lb, w, lane, r);
+        chains<2, M == kGeneral>(lds, lb, w, lane, r);
       } else {
-        r[0] = chain_fold(lds, lb, w[0], lane);
+        r[0] = chain_fold<M>(lds, lb, w[0], lane);
       }
       if (M == kGeneral) {  // buffers of < 4 bytes: bytewise, replacing the (unused) chain
         if (p0.bi.len < 4) r[0] = ~tiny_crc(lds, p0.bi);
@@ -898,6 +923,10 @@ template <int M>
 __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   if constexpr (M == kAligned) {
+#if defined(NVL_DIAG_ONLY_PAIRS)  // ISA inspection of scheduler A alone
+    run_pairs<NVL_FAST_U>(g, ka, lds);
+    return;
+#endif
     if (g.J == 1) {
       run_pairs<NVL_FAST_U>(g, ka, lds);
       return;

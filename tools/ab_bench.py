@@ -4,7 +4,7 @@
 Each .so is a full build of the C ABI; all run the config-2 fast path
 (10^5 x 4 KiB) on the same device buffer, M rounds x R reps, HIP-event timed.
 """
-import ctypes, os, sys, json
+import ctypes, os, sys, json, time
 import numpy as np
 import torch
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.getcwd()))
@@ -34,6 +34,7 @@ def main():
                                           ws.data_ptr(), ws.numel(), st)
         assert rc == 0
     times = [[] for _ in libs]
+    walls = [[] for _ in libs]  # us per step of `reps` back-to-back launches, no events
     for k in range(len(libs)):
         for _ in range(3): run(k)
     torch.cuda.synchronize()
@@ -44,12 +45,18 @@ def main():
                 ev[2*j].record(); run(k); ev[2*j+1].record()
             torch.cuda.synchronize()
             times[k] += [ev[2*j].elapsed_time(ev[2*j+1]) * 1e3 for j in range(reps)]
+            t0 = time.perf_counter()
+            for j in range(reps):
+                run(k)
+            torch.cuda.synchronize()
+            walls[k].append((time.perf_counter() - t0) / reps * 1e6)
     ref = outs[0].cpu()
     for k, p in enumerate(paths):
         t = np.array(times[k]); same = bool(torch.equal(outs[k].cpu(), ref))
         gbs = n * (L + 4) / (np.median(t) * 1e-6) / 1e9
         print(json.dumps({"variant": os.path.basename(p), "median_us": round(float(np.median(t)), 2),
                           "min_us": round(float(t.min()), 2), "GB/s": round(gbs, 1), "frac": round(gbs / 8000, 4),
+                          "wall_us_per_step": round(float(np.median(walls[k])), 2),
                           "same_as_first": same}))
 
 main()

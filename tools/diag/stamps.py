@@ -36,3 +36,9 @@ for c in sorted(set(cnt.tolist())):
 for x in range(8):
     m = xcc == x
     print(f"xcc {x}: waves {m.sum():4d} start p50 {np.median(start[m]):6.2f} max {start[m].max():6.2f} fill p50 {np.median(fill[m]):6.2f} end p50 {np.median(end[m]):6.2f} min {end[m].min():6.2f} max {end[m].max():6.2f}")
+# per-workgroup view (16 waves per workgroup): spread inside a CU vs across CUs
+wg = end.reshape(-1, 16)
+wg_max, wg_min = wg.max(1), wg.min(1)
+print("per-WG end spread (max-min) us p10/p50/p90:", " ".join(f"{x:.2f}" for x in np.percentile(wg_max - wg_min, [10, 50, 90])))
+print("per-WG last-wave end us p0/p10/p50/p90/p100:", " ".join(f"{x:.2f}" for x in np.percentile(wg_max, [0, 10, 50, 90, 100])))
+print("per-WG first-wave end us p0/p50/p100:", " ".join(f"{x:.2f}" for x in np.percentile(wg_min, [0, 50, 100])))

@@ -9,7 +9,7 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
 echo "[gpu_check] $(date) start tag=$TAG"
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
 rc=$?; echo "[gpu_check] pytest rc=$rc"; tail -3 $OUT/pytest_gpu_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1

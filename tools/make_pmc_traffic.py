@@ -24,7 +24,7 @@ cover = mean["SQ_WAVES"] / launched_waves
 fetch = mean["FETCH_SIZE"] * 1024 * 2 / cover
 write = mean.get("WRITE_SIZE", 0.0) * 1024 / cover
 alg = blocks * (4096 + 4)
-res = {"kernel": "crc32c_fixed_kernel<true>", "blocks": blocks, "block_bytes": 4096,
+res = {"kernel": "crc32c_fixed_kernel<0>", "blocks": blocks, "block_bytes": 4096,
        "hbm_bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
        "alg_bytes_per_launch": alg, "traffic_over_alg": round((fetch + write) / alg, 4),
        "raw": {"FETCH_SIZE_KiB": mean["FETCH_SIZE"], "WRITE_SIZE_KiB": mean.get("WRITE_SIZE"),

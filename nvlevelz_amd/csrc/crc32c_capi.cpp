@@ -10,6 +10,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/nvl_crc32c.h"
@@ -43,10 +44,69 @@ struct DeviceState {
   int num_cu = 0;
   uint32_t* tables = nullptr;
   int status = NVL_CRC32C_OK;  // OK, or why the backend is unusable
+  std::mutex cmu;
+  std::unordered_map<hipStream_t, uint32_t*> counters;  // per-stream counter blocks
 };
 
 std::mutex g_mu;
 std::atomic<DeviceState*> g_state[kMaxDevices];
+std::atomic<uint64_t> g_generation{1};  // bumped by shutdown: invalidates the per-thread cache
+
+// Streams that get a counter block; launches on further streams run the
+// unfused pipeline (plan, kernel, fix-up).
+constexpr size_t kMaxCounterStreams = 4096;
+
+// The counter block of `st` (LaunchCtx::counter), created zeroed on first
+// use (a hipMemsetAsync on `st`, so it is ordered before the first launch);
+// nullptr when unavailable.  Lock-free after a thread's first launch on a
+// stream.
+uint32_t* counters_for(DeviceState* s, hipStream_t st) {
+  struct Cache {
+    uint64_t gen = 0;
+    DeviceState* s = nullptr;
+    hipStream_t st = nullptr;
+    uint32_t* c = nullptr;
+  };
+  thread_local Cache cache;
+  const uint64_t gen = g_generation.load(std::memory_order_acquire);
+  if (cache.gen == gen && cache.s == s && cache.st == st && cache.c) return cache.c;
+  std::lock_guard<std::mutex> lk(s->cmu);
+  auto it = s->counters.find(st);
+  uint32_t* c = it == s->counters.end() ? nullptr : it->second;
+  if (!c) {
+    if (s->counters.size() >= kMaxCounterStreams) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, kCounterBytes) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, kCounterBytes, st) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    c = static_cast<uint32_t*>(p);
+    s->counters[st] = c;
+  }
+  cache = Cache{gen, s, st, c};
+  return c;
+}
+
+// One non-blocking stream per calling thread for the host-resident entry
+// points (a stream per call would also mean a counter block per call).
+hipStream_t thread_stream(int device) {
+  struct TS {
+    int device = -1;
+    hipStream_t st = nullptr;
+  };
+  thread_local TS ts[4];
+  for (auto& t : ts)
+    if (t.st && t.device == device) return t.st;
+  for (auto& t : ts) {
+    if (!t.st) {
+      if (hipStreamCreateWithFlags(&t.st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+      t.device = device;
+      return t.st;
+    }
+  }
+  return nullptr;
+}
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -134,7 +194,7 @@ int do_fixed(DeviceState* s, const void* base, uint64_t stride, uint64_t len, ui
   } else if (need && ws_bytes < need) {
     return NVL_CRC32C_ENOSPC;
   }
-  LaunchCtx lc{st, s->num_cu, s->tables};
+  LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   hipError_t e = launch_fixed(lc, static_cast<const uint8_t*>(base), stride, len, n, init, init_all, out, flags,
                               static_cast<Rec*>(ws));
   if (own) (void)hipFreeAsync(ws, st);
@@ -162,8 +222,17 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   uint64_t* unit_first = reinterpret_cast<uint64_t*>(w + off_map);
   Rec* recs = reinterpret_cast<Rec*>(w + off_recs);
   void* tmp = w + off_tmp;
-  LaunchCtx lc{st, s->num_cu, s->tables};
+  LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   const bool small = var_plan_small(n);
+#if !defined(NVL_NO_FUSED)
+  if (small && s->num_cu <= 4096) lc.counter = counters_for(s, st);
+  if (lc.counter) {
+    hipError_t ef = launch_var_fused(lc, static_cast<const uint8_t*>(base), offsets, lengths, n, init, init_all, out,
+                                     flags, recs);
+    if (own) (void)hipFreeAsync(ws, st);
+    return hip_rc(ef);
+  }
+#endif
   hipError_t e;
   if (small) {
     e = launch_var_plan_small(lc, lengths, n, cs, unit_first);
@@ -293,6 +362,7 @@ int nvl_crc32c_init(int device) {
 
 int nvl_crc32c_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
+  g_generation.fetch_add(1, std::memory_order_acq_rel);
   for (int d = 0; d < kMaxDevices; ++d) {
     DeviceState* s = g_state[d].exchange(nullptr);
     if (s) {
@@ -301,6 +371,7 @@ int nvl_crc32c_shutdown(void) {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(d);
         (void)hipFree(s->tables);
+        for (auto& kv : s->counters) (void)hipFree(kv.second);
         if (prev >= 0) (void)hipSetDevice(prev);
       }
       delete s;
@@ -386,16 +457,13 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
     hini[i] = init ? init[i] : init_all;
     pos += align_up(lengths[i], 16);
   }
-  hipStream_t st;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
+  hipStream_t st = thread_stream(s->device);
+  if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
   size_t off_cs, off_map, off_recs, off_tmp;
   const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_tmp);
   const size_t dbytes = total + n * 4 + ws + 512;
-  if (hipMallocAsync(&d, dbytes, st) != hipSuccess) {
-    (void)hipStreamDestroy(st);
-    return NVL_CRC32C_EHIP;
-  }
+  if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
   void* dws = d + align_up(total, 256) + align_up(n * 4, 256);
   hipError_t e = hipMemcpyAsync(d, hst, total, hipMemcpyHostToDevice, st);
@@ -407,7 +475,6 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
   if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
-  (void)hipStreamDestroy(st);
   return rc;
 }
 
@@ -440,16 +507,13 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     hlen[i] = lengths[i];
     hini[i] = init ? init[i] : init_all;
   }
-  hipStream_t st;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
+  hipStream_t st = thread_stream(s->device);
+  if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
   size_t off_cs, off_map, off_recs, off_tmp;
   const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_tmp);
   const size_t dbytes = align_up(total, 256) + align_up(n * 4, 256) + ws + 256;
-  if (hipMallocAsync(&d, dbytes, st) != hipSuccess) {
-    (void)hipStreamDestroy(st);
-    return NVL_CRC32C_EHIP;
-  }
+  if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
   void* dws = d + align_up(total, 256) + align_up(n * 4, 256);
   hipError_t e = hipMemcpyAsync(d, hst, total, hipMemcpyHostToDevice, st);
@@ -461,7 +525,6 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
   if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
-  (void)hipStreamDestroy(st);
   return rc;
 }
 

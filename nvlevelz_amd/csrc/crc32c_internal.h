@@ -26,10 +26,16 @@ struct Rec {
 constexpr unsigned long long kNoBuf = ~0ull;
 constexpr uint32_t kRecEnds = 0x80000000u;
 
+// Per-stream counter block: kCounterBytes, zeroed once when created; every
+// kernel that counts in it leaves it zero again, so the launches of one
+// stream (ordered) share it.
+constexpr size_t kCounterBytes = 256;
+
 struct LaunchCtx {
   hipStream_t stream;
   int num_cu;
   const uint32_t* tables;  // device blob
+  uint32_t* counter;       // the stream's counter block (fused kernels), or nullptr
 };
 
 void build_device_tables(uint32_t* words /* kTableWords */);
@@ -50,6 +56,12 @@ hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt,
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
                       uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, bool have_unit_map);
+
+// Plan + checksum + fix-up in one launch (n <= kPlanSmallMax, lc.counter
+// set); recs: the launch_var workspace records (hold the edge records).
+hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
+                            uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
+                            Rec* recs);
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

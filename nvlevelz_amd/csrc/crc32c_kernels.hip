@@ -44,6 +44,7 @@ constexpr int kWave = 64;
 constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWave * kWavesPerWG;  // 1024
 constexpr uint32_t kChunk = 4096;
+constexpr uint32_t kUnitsPerWG = 64;  // work units per workgroup (scheduler B)
 
 // LDS image (bytes)
 // The operator tables sit first so that every table offset of a lookup fits
@@ -255,6 +256,37 @@ struct BufInfo {
   uint32_t s;        // ~init, injected into the first 4 bytes
 };
 
+// Wave-uniform reads of read-only metadata (lengths, offsets, init, plan
+// arrays) through the constant address space: scalar loads (s_load, counted
+// in lgkmcnt).  As vector loads they were counted in vmcnt, whose in-order
+// retirement made every buffer boundary wait for the prefetched chunk too.
+// (Written before the launch only: the scalar cache is invalidated at kernel
+// start, cdna_hip_programming.md Guideline 16 Pitfall 6.)
+template <class T>
+__device__ __forceinline__ T ldc(const T* p, uint64_t i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
+struct KArgs {
+  uint32_t* out;
+  uint32_t flags;
+  Rec* recs;  // 2 per work unit: [2u] = head portion, [2u+1] = tail portion (or nullptr)
+  const uint32_t* tables;
+  uint32_t* counter;  // the stream's done counter (fused variable kernel); zero between launches
+};
+
+// Global work units: the grid's NU = gridDim.x * kUnitsPerWG units split the
+// chunk space [0, T) evenly; workgroup b owns units [64b, 64b+64).
+__device__ __forceinline__ uint64_t global_unit_lo(uint64_t T, uint32_t u) {
+  return T * (uint64_t)u / ((uint64_t)gridDim.x * kUnitsPerWG);
+}
+__device__ __forceinline__ void global_put_recs(const KArgs& ka, uint32_t u, const Rec& h, const Rec& t) {
+  if (ka.recs) {
+    ka.recs[2 * (uint64_t)u] = h;
+    ka.recs[2 * (uint64_t)u + 1] = t;
+  }
+}
+
 struct FixedGeom {
   const uint8_t* base;
   uint64_t stride, len, n;
@@ -267,11 +299,15 @@ struct FixedGeom {
     c = (uint32_t)(t - i * J);
   }
   __device__ __forceinline__ BufInfo info(uint64_t i) const {
-    const uint32_t ini = init ? init[i] : init_all;
+    const uint32_t ini = init ? ldc(init, i) : init_all;
     return BufInfo{base + i * stride, len, J, ~ini};
   }
   __device__ __forceinline__ void locate_unit(uint32_t, uint64_t t, uint64_t& i, uint32_t& c) const {
     locate(t, i, c);
+  }
+  __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo(T, u); }
+  __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
+    global_put_recs(ka, u, h, t);
   }
 };
 
@@ -284,7 +320,7 @@ struct VarGeom {
   uint64_t n;
   const uint32_t* init;
   uint32_t init_all;
-  __device__ __forceinline__ uint64_t total() const { return chunk_start[n]; }
+  __device__ __forceinline__ uint64_t total() const { return ldc(chunk_start, n); }
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
     uint64_t lo = 0, hi = n;  // invariant: chunk_start[lo] <= t < chunk_start[hi]
     while (hi - lo > 1) {
@@ -296,14 +332,18 @@ struct VarGeom {
   }
   // Start of work unit u (chunk t = its first): one load instead of a search.
   __device__ __forceinline__ void locate_unit(uint32_t u, uint64_t t, uint64_t& i, uint32_t& c) const {
-    i = unit_first[u];
-    c = (uint32_t)(t - chunk_start[i]);
+    i = ldc(unit_first, u);
+    c = (uint32_t)(t - ldc(chunk_start, i));
   }
   __device__ __forceinline__ BufInfo info(uint64_t i) const {
-    const uint64_t L = lengths[i];
+    const uint64_t L = ldc(lengths, i);
     const uint32_t J = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
-    const uint32_t ini = init ? init[i] : init_all;
-    return BufInfo{base + offsets[i], L, J, ~ini};
+    const uint32_t ini = init ? ldc(init, i) : init_all;
+    return BufInfo{base + ldc(offsets, i), L, J, ~ini};
+  }
+  __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo(T, u); }
+  __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
+    global_put_recs(ka, u, h, t);
   }
 };
 
@@ -594,12 +634,6 @@ __device__ __forceinline__ uint32_t tiny_crc(const uint8_t* lds, const BufInfo& 
   return ~l;
 }
 
-struct KArgs {
-  uint32_t* out;
-  uint32_t flags;
-  Rec* recs;  // 2 per work unit: [2u] = head portion, [2u+1] = tail portion (or nullptr)
-  const uint32_t* tables;
-};
 
 // Position of one chunk.
 struct Pos {
@@ -787,7 +821,6 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
 // boundary leaves a head/tail record for crc32c_fixup_kernel.  The next
 // chunk -- including the first chunk of the next unit -- is always in flight
 // while the current one computes.
-constexpr uint32_t kUnitsPerWG = 64;
 #ifndef NVL_UNIT_STEP
 #define NVL_UNIT_STEP 1  // chunks per step in scheduler B (2: interleaved pair; A/B'd, no gain)
 #endif
@@ -799,9 +832,8 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t T = g.total();
-  const uint64_t NU = (uint64_t)gridDim.x * kUnitsPerWG;
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
-  auto lo_of = [&](uint32_t uu) -> uint64_t { return T * (uint64_t)uu / NU; };
+  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.unit_lo(T, uu); };
 
   // One flat loop over steps.  A step is the next two chunks of the current
   // unit u (one at an odd tail; none when u is empty), their chains
@@ -884,10 +916,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
         if (st.from_zero) tail = Rec{last_i, st.acc, st.cnt};
         else st.head = Rec{last_i, st.acc, st.cnt};
       }
-      if (ka.recs && lane == 0) {
-        ka.recs[2 * (uint64_t)u] = st.head;
-        ka.recs[2 * (uint64_t)u + 1] = tail;
-      }
+      if (lane == 0) g.put_recs(ka, lds, u, st.head, tail);
       if (un >= ub1) break;
       u = un;
       t = un_lo;
@@ -1052,13 +1081,11 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t
   }
 }
 
-// Fold the per-unit records of buffers cut by work-unit boundaries.  One
-// thread per unit; the unit where a buffer ENDS walks back over earlier units.
-__global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
-                                    const uint32_t* __restrict__ tables, uint32_t* __restrict__ out,
-                                    uint32_t flags) {
-  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= nw) return;
+// Fold the per-unit records of buffers cut by work-unit boundaries: unit w's
+// head record, if it holds the LAST portion of a buffer, walks back over
+// earlier units for the buffer's other portions.
+__device__ __forceinline__ void fixup_unit(const Rec* __restrict__ recs, uint32_t w, const uint32_t* __restrict__ tables,
+                                           uint32_t* __restrict__ out, uint32_t flags) {
   const Rec h = recs[2 * w];
   if (h.buf == kNoBuf || !(h.cnt & kRecEnds)) return;
   const uint32_t* x2n = tables + kGX2n;
@@ -1082,6 +1109,300 @@ __global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
     if (hx.buf != kNoBuf || tx.buf != kNoBuf) break;  // unreachable for a consistent plan
   }
   out[h.buf] = finish(~total, flags);
+}
+
+// One thread per unit.
+__global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
+                                    const uint32_t* __restrict__ tables, uint32_t* __restrict__ out,
+                                    uint32_t flags) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < nw) fixup_unit(recs, w, tables, out, flags);
+}
+
+// ---------------------------------------------------------------------------
+// Fused variable-length batch (n <= kPlanSmallMax): plan, checksum and fix-up
+// in ONE launch instead of three (config 3: plan 26 + kernel 255 + fix-up
+// 7 us, plus two launch gaps).
+//   * Plan prologue, in the LDS the tables later occupy: every workgroup
+//     scans all n chunk counts (n * 8 B, L2-resident after the first reader):
+//     coalesced counts, run-relative prefixes, block scan.  Workgroup b owns
+//     chunks [T*b/G, T*(b+1)/G), cut into 64 work units whose (buffer, chunk)
+//     starts 64 threads find by binary search.
+//   * Records of buffers cut by unit boundaries stay in LDS and the workgroup
+//     folds them itself.  A buffer crossing a WORKGROUP boundary leaves edge
+//     records: E_in, its portion here when it began in an earlier workgroup
+//     (flagged when it also ends here), and E_out, the portion of a buffer
+//     that begins here and runs on.  Hand-off per MI355X_MICROARCH.md's
+//     visibility table, row 1 (cdna_hip_programming.md Guideline 16): edge
+//     records stored sc1 (agent-scope atomic stores), the storing wave drains
+//     (vmcnt(0)), ONE lane adds to the stream's done counter; the workgroup
+//     whose add returns G-1 reads every edge record with sc1 loads, folds the
+//     cross-workgroup buffers and re-zeroes the counter (zeroed when the
+//     stream's counter was created; every launch leaves it zero).
+constexpr uint32_t kUnitOff = kLdsBytes;                                           // u32 ubuf[64], uc[64]
+constexpr uint32_t kRecOff = kUnitOff + 2u * kUnitsPerWG * 4u;                     // Rec[2 * 64]
+constexpr uint32_t kEdgeOff = kRecOff + 2u * kUnitsPerWG * (uint32_t)sizeof(Rec);  // Rec e_in, e_out; u32 last
+constexpr uint32_t kFusedLdsBytes = kEdgeOff + 2u * (uint32_t)sizeof(Rec) + 16u;
+static_assert(kFusedLdsBytes <= 160u * 1024u, "fused LDS image exceeds 160 KiB");
+constexpr uint32_t kPlanJsBytes = (uint32_t)(kPlanSmallMax + kPlanSmallMax / 32) * 4u;
+constexpr uint32_t kPlanWsumOff = kPlanJsBytes;             // u64 [16]
+constexpr uint32_t kPlanRunOff = kPlanWsumOff + 16u * 8u;   // u64 run starts [1024]
+static_assert(kPlanRunOff + 1024u * 8u <= kSliceOff + kRepBytes, "plan scratch must fit under the table image");
+constexpr uint32_t kMaxFusedGrid = 4096;  // the last workgroup folds 2 edge records per workgroup in LDS
+static_assert(2u * kMaxFusedGrid * sizeof(Rec) <= kSliceOff + kRepBytes, "edge fold must fit under the table image");
+
+struct VarGeomFused {
+  const uint8_t* base;
+  const uint64_t* offsets;
+  const uint64_t* lengths;
+  uint64_t n;
+  const uint32_t* init;
+  uint32_t init_all;
+  uint64_t C0, C1;        // this workgroup's chunk range
+  const uint32_t* ubuf;   // LDS: buffer holding the first chunk of local unit k
+  const uint32_t* uc;     // LDS: that chunk's index within the buffer
+  uint32_t ub0;
+  __device__ __forceinline__ uint64_t total() const { return C1 - C0; }
+  __device__ __forceinline__ uint64_t unit_lo(uint64_t span, uint32_t u) const {
+    return C0 + span * (uint64_t)(u - ub0) / kUnitsPerWG;
+  }
+  __device__ __forceinline__ void locate_unit(uint32_t u, uint64_t, uint64_t& i, uint32_t& c) const {
+    i = ubuf[u - ub0];
+    c = uc[u - ub0];
+  }
+  __device__ __forceinline__ BufInfo info(uint64_t i) const {
+    const uint64_t L = ldc(lengths, i);
+    const uint32_t J = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
+    const uint32_t ini = init ? ldc(init, i) : init_all;
+    return BufInfo{base + ldc(offsets, i), L, J, ~ini};
+  }
+  __device__ __forceinline__ void put_recs(const KArgs&, uint8_t* lds, uint32_t u, const Rec& h, const Rec& t) const {
+    Rec* r = reinterpret_cast<Rec*>(lds + kRecOff);
+    r[2 * (u - ub0)] = h;
+    r[2 * (u - ub0) + 1] = t;
+  }
+};
+
+#if defined(NVL_DIAG_FUSED)
+__device__ unsigned long long g_fstamps[8 * 1024];
+#define NVL_FSTAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_fstamps[8 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define NVL_FSTAMP(k) do {} while (0)
+#endif
+
+// Plan prologue.  After it: LDS holds ubuf/uc for the 64 local units, and
+// C0/C1 (returned) bound the workgroup's chunk range.
+template <int NW>
+__device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restrict__ lengths, uint32_t nn,
+                                           uint64_t& C0, uint64_t& C1) {
+  constexpr uint32_t kT = kWave * NW;
+  static_assert(kT == 1024, "plan layout assumes 1024 threads");
+  constexpr int kPer = (int)(kPlanSmallMax / kT);
+  uint32_t* js = reinterpret_cast<uint32_t*>(lds);
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(lds + kPlanWsumOff);
+  uint64_t* rstart = reinterpret_cast<uint64_t*>(lds + kPlanRunOff);
+  uint32_t* ubuf = reinterpret_cast<uint32_t*>(lds + kUnitOff);
+  uint32_t* uc = ubuf + kUnitsPerWG;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  {  // chunk counts, all of the thread's lengths in flight at once
+    uint64_t Ls[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = t + (uint32_t)k * kT;
+      Ls[k] = i < nn ? lengths[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = t + (uint32_t)k * kT;
+      if (i < nn) js[plan_pad(i)] = Ls[k] <= kChunk ? 1u : (uint32_t)((Ls[k] + kChunk - 1) / kChunk);
+    }
+  }
+  __syncthreads();
+  NVL_FSTAMP(4);
+  const uint32_t per = (nn + kT - 1) / kT;
+  const uint32_t i0 = min(nn, t * per), i1 = min(nn, i0 + per);
+  uint32_t sum = 0;  // run-relative exclusive prefixes in place
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t j = js[plan_pad(i)];
+    js[plan_pad(i)] = sum;
+    sum += j;
+  }
+  uint64_t x = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  NVL_FSTAMP(5);
+  __syncthreads();
+  uint64_t before = 0, T = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < (uint32_t)NW; ++v) {
+    const uint64_t sv = wsum[v];
+    before += v < wv ? sv : 0;
+    T += sv;
+  }
+  rstart[t] = before + x - sum;  // chunk_start of the run's first buffer (runs past n: T)
+  __syncthreads();
+  NVL_FSTAMP(6);
+  // chunk_start of the buffer holding chunk q (q < T): last run r with
+  // rstart[r] <= q (empty runs share their successor's start, so take the
+  // last), then the last buffer of the run whose start is <= q.
+  auto buf_of = [&](uint64_t q, uint64_t& cs) -> uint32_t {
+    uint32_t lo = 0, hi = kT;  // rstart[lo] <= q < rstart[hi] (rstart[kT] := inf)
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rstart[mid] <= q) lo = mid; else hi = mid;
+    }
+    const uint64_t r0 = rstart[lo];
+    uint32_t a = lo * per, b = min(nn, a + per);  // js[a] = 0 <= q - r0
+    while (b - a > 1) {
+      const uint32_t mid = (a + b) >> 1;
+      if (r0 + js[plan_pad(mid)] <= q) a = mid; else b = mid;
+    }
+    cs = r0 + js[plan_pad(a)];
+    return a;
+  };
+  // T is the same in every lane: keep it and the range in SGPRs (as VGPRs
+  // they stayed live through the main loop, which then spilled).
+  T = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(T >> 32)) << 32) |
+      __builtin_amdgcn_readfirstlane((uint32_t)T);
+  C0 = T * blockIdx.x / gridDim.x;
+  C1 = T * (blockIdx.x + 1) / gridDim.x;
+  if (t < kUnitsPerWG) {
+    const uint64_t q = C0 + (C1 - C0) * t / kUnitsPerWG;
+    if (q < C1) {
+      uint64_t cs;
+      ubuf[t] = buf_of(q, cs);
+      uc[t] = (uint32_t)(q - cs);
+    }
+  }
+  __syncthreads();
+}
+
+// Fold the earlier portions of buffer `buf` (LDS records of units x < k)
+// into (total, after): middle portions are head records, the first portion a
+// tail record.  True when the first portion is in this workgroup.
+__device__ __forceinline__ bool fold_back(const Rec* lr, int k, unsigned long long buf, uint32_t& total,
+                                          uint64_t& after, const uint32_t* x2n) {
+  for (int x = k - 1; x >= 0; --x) {
+    const Rec hx = lr[2 * x];
+    if (hx.buf == buf) {
+      total ^= nvl::shift_bytes(x2n, hx.raw, after * kChunk);
+      after += hx.cnt & ~kRecEnds;
+      continue;
+    }
+    const Rec tx = lr[2 * x + 1];
+    if (tx.buf == buf) {
+      total ^= nvl::shift_bytes(x2n, tx.raw, after * kChunk);
+      after += tx.cnt;
+      return true;
+    }
+    if (hx.buf != kNoBuf || tx.buf != kNoBuf) return false;  // unreachable for a consistent plan
+  }
+  return false;
+}
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+// Edge records as two 8-B agent-scope atomic accesses (sc1 stores / loads).
+__device__ __forceinline__ void store_edge(gu64* g, const Rec& r) {
+  __hip_atomic_store(g, r.buf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, (unsigned long long)r.raw | ((unsigned long long)r.cnt << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Rec load_edge(gu64* g) {
+  const unsigned long long b = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long v = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return Rec{b, (uint32_t)v, (uint32_t)(v >> 32)};
+}
+
+__global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(VarGeom gv, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes];
+  NVL_FSTAMP(0);
+  const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
+  uint64_t C0, C1;
+  fused_plan<kGenWaves>(lds, gv.lengths, (uint32_t)gv.n, C0, C1);
+  NVL_FSTAMP(1);
+  const uint32_t* ubuf = reinterpret_cast<const uint32_t*>(lds + kUnitOff);
+  const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,
+                       ubuf + kUnitsPerWG, ub0};
+  run_units<kGeneral, kGenWaves>(g, ka, lds);
+  NVL_FSTAMP(2);
+  const uint32_t* x2n = ka.tables + kGX2n;
+  const Rec* lr = reinterpret_cast<const Rec*>(lds + kRecOff);
+  Rec* edge = reinterpret_cast<Rec*>(lds + kEdgeOff);
+  uint32_t* last = reinterpret_cast<uint32_t*>(lds + kEdgeOff + 2u * sizeof(Rec));
+  const uint32_t t = threadIdx.x;
+  if (t < 2) edge[t] = Rec{kNoBuf, 0u, 0u};
+  __syncthreads();  // every unit's records are in LDS
+  if (t < kUnitsPerWG) {  // a buffer that ends in unit t and began in an earlier unit
+    const Rec h = lr[2 * t];
+    if (h.buf != kNoBuf && (h.cnt & kRecEnds)) {
+      uint32_t total = h.raw;
+      uint64_t after = h.cnt & ~kRecEnds;
+      if (fold_back(lr, (int)t, h.buf, total, after, x2n)) ka.out[h.buf] = finish(~total, ka.flags);
+      else edge[0] = Rec{h.buf, total, (uint32_t)after | kRecEnds};  // began before C0
+    }
+  } else if (t == kUnitsPerWG) {  // the buffer of the range's last chunk, if it runs past C1
+    int L = (int)kUnitsPerWG - 1;
+    while (L >= 0 && lr[2 * L].buf == kNoBuf && lr[2 * L + 1].buf == kNoBuf) --L;
+    if (L >= 0) {
+      const Rec h = lr[2 * L], tl = lr[2 * L + 1];
+      if (tl.buf != kNoBuf) {
+        edge[1] = tl;
+      } else if (!(h.cnt & kRecEnds)) {  // a middle portion: the buffer covers unit L
+        uint32_t total = h.raw;
+        uint64_t after = h.cnt;
+        if (fold_back(lr, L, h.buf, total, after, x2n)) edge[1] = Rec{h.buf, total, (uint32_t)after};
+        else edge[0] = Rec{h.buf, total, (uint32_t)after};  // began before C0 and runs past C1
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {  // publish: sc1 stores, drain, ONE counter add
+    gu64* eg = (gu64*)ka.recs + 4ull * blockIdx.x;
+    store_edge(eg, edge[0]);
+    store_edge(eg + 2, edge[1]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t d = __hip_atomic_fetch_add((gu32*)ka.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = d == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  NVL_FSTAMP(3);
+  if (!*last) return;
+  // The last workgroup: every edge record (sc1 loads) into the now free table
+  // image, then one thread per workgroup whose E_in ends a buffer folds it
+  // back through the earlier workgroups' edge records.
+  const uint32_t G = gridDim.x;
+  Rec* E = reinterpret_cast<Rec*>(lds);  // [2b] = E_in of workgroup b, [2b+1] = E_out
+  gu64* eg = (gu64*)ka.recs;
+  for (uint32_t b = t; b < 2 * G; b += blockDim.x) E[b] = load_edge(eg + 2ull * b);
+  __syncthreads();
+  for (uint32_t b = t; b < G; b += blockDim.x) {
+    const Rec e = E[2 * b];
+    if (e.buf == kNoBuf || !(e.cnt & kRecEnds)) continue;
+    uint32_t total = e.raw;
+    uint64_t after = e.cnt & ~kRecEnds;
+    for (int bb = (int)b - 1; bb >= 0; --bb) {
+      const Rec ei = E[2 * bb], eo = E[2 * bb + 1];
+      if (ei.buf == e.buf) {  // a workgroup wholly inside the buffer
+        total ^= nvl::shift_bytes(x2n, ei.raw, after * kChunk);
+        after += ei.cnt;
+        continue;
+      }
+      if (eo.buf == e.buf) {  // the workgroup where it began
+        total ^= nvl::shift_bytes(x2n, eo.raw, after * kChunk);
+        break;
+      }
+      if (ei.buf != kNoBuf || eo.buf != kNoBuf) break;  // unreachable for a consistent plan
+    }
+    ka.out[e.buf] = finish(~total, ka.flags);
+  }
+  if (t == 0) (void)__hip_atomic_exchange((gu32*)ka.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Synthetic stream: one thread per 8-byte word.
@@ -1139,7 +1460,7 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   const uint32_t grid = grid_for(lc.num_cu, n * (uint64_t)J);
   const bool aligned = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
-  dev::KArgs ka{out, flags, J > 1 ? recs : nullptr, lc.tables};
+  dev::KArgs ka{out, flags, J > 1 ? recs : nullptr, lc.tables, nullptr};
   if (aligned)
     hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
                        ka);
@@ -1160,6 +1481,11 @@ size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
 size_t var_recs_bytes(int num_cu) { return 2ull * (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(Rec); }
 size_t var_unit_map_bytes(int num_cu) { return (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(uint64_t); }
 
+#if defined(NVL_DIAG_FUSED)
+extern "C" __attribute__((visibility("default"))) int nvl_diag_fstamps(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_fstamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
 #if defined(NVL_DIAG_STAMPS)
 extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned long long* host, size_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
@@ -1167,6 +1493,18 @@ extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned l
 #endif
 
 bool var_plan_small(uint64_t n) { return n <= dev::kPlanSmallMax; }
+
+hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
+                            uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
+                            Rec* recs) {
+  if (n == 0) return hipSuccess;
+  if (n > dev::kPlanSmallMax || !lc.counter || lc.num_cu > (int)dev::kMaxFusedGrid) return hipErrorInvalidValue;
+  dev::VarGeom g{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
+  dev::KArgs ka{out, flags, recs, lc.tables, lc.counter};
+  hipLaunchKernelGGL(dev::crc32c_var_fused_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kWave * dev::kGenWaves), 0,
+                     lc.stream, g, ka);
+  return hipGetLastError();
+}
 
 hipError_t launch_var_plan_small(const LaunchCtx& lc, const uint64_t* lengths, uint64_t n, uint64_t* chunk_start,
                                  uint64_t* unit_first) {
@@ -1196,7 +1534,7 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
     if (e0 != hipSuccess) return e0;
   }
   dev::VarGeom g{base, offsets, lengths, chunk_start, unit_first, n, init, init_all};
-  dev::KArgs ka{out, flags, recs, lc.tables};
+  dev::KArgs ka{out, flags, recs, lc.tables, nullptr};
   hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0, lc.stream, g, ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -1193,6 +1193,11 @@ __device__ unsigned long long g_fstamps[8 * 1024];
 
 // Plan prologue.  After it: LDS holds ubuf/uc for the 64 local units, and
 // C0/C1 (returned) bound the workgroup's chunk range.
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 template <int NW>
 __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restrict__ lengths, uint32_t nn,
                                            uint64_t& C0, uint64_t& C1) {
@@ -1267,8 +1272,7 @@ __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restr
   };
   // T is the same in every lane: keep it and the range in SGPRs (as VGPRs
   // they stayed live through the main loop, which then spilled).
-  T = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(T >> 32)) << 32) |
-      __builtin_amdgcn_readfirstlane((uint32_t)T);
+  T = uniform_u64(T);
   C0 = T * blockIdx.x / gridDim.x;
   C1 = T * (blockIdx.x + 1) / gridDim.x;
   if (t < kUnitsPerWG) {
@@ -1326,6 +1330,11 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1;
   fused_plan<kGenWaves>(lds, gv.lengths, (uint32_t)gv.n, C0, C1);
+  // The range is uniform, but the 64-bit divisions that made it ran on the
+  // VALU: pin it to SGPRs, or it stays in VGPRs through the main loop and
+  // that spills (25 VGPRs, 108 B/lane scratch, cfg3 287 -> 430 us).
+  C0 = uniform_u64(C0);
+  C1 = uniform_u64(C1);
   NVL_FSTAMP(1);
   const uint32_t* ubuf = reinterpret_cast<const uint32_t*>(lds + kUnitOff);
   const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,

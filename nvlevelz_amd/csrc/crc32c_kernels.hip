@@ -560,12 +560,25 @@ __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, c
   }
   return;
 #endif
+#if defined(NVL_ABL_HALF)  // ablation: two independent 8-step half chains per lane (wrong combine)
+  if constexpr (U == 1) {
+    uint32_t a = w[0][0], b = w[0][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a = slice4_next(lds, a, k < 7 ? w[0][k + 1] : 0u, lb);
+      b = slice4_next(lds, b, k < 7 ? w[0][k + 9] : 0u, lb);
+    }
+    crc[0] = a ^ b;
+  } else
+#endif
+  {
 #pragma unroll
   for (int u = 0; u < U; ++u) crc[u] = w[u][0];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
 #pragma unroll
     for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+  }
   }
 #if defined(NVL_ABL_NOFOLD)  // ablation: chains only, no butterfly
 #pragma unroll
@@ -824,11 +837,14 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
 #ifndef NVL_UNIT_STEP
 #define NVL_UNIT_STEP 1  // chunks per step in scheduler B (2: interleaved pair; A/B'd, no gain)
 #endif
-constexpr int kStep = NVL_UNIT_STEP;
+#ifndef NVL_UNIT_STEP_ALIGNED
+#define NVL_UNIT_STEP_ALIGNED 2  // the same for the aligned (kAligned, J > 1) kernel: no spills there (cfg4 -3 %)
+#endif
 
 template <int M, int NW, class G>
 __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
+  constexpr int kStep = M == kAligned ? NVL_UNIT_STEP_ALIGNED : NVL_UNIT_STEP;
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t T = g.total();
@@ -1412,6 +1428,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     ka.out[e.buf] = finish(~total, ka.flags);
   }
   if (t == 0) (void)__hip_atomic_exchange((gu32*)ka.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  NVL_FSTAMP(7);
 }
 
 // Synthetic stream: one thread per 8-byte word.

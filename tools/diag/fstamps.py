@@ -22,14 +22,23 @@ st = torch.cuda.current_stream().cuda_stream
 for _ in range(5):
     assert lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0, ws.data_ptr(), wsb, st) == 0
 torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+assert lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0, ws.data_ptr(), wsb, st) == 0
+e1.record()
+torch.cuda.synchronize()
+print("event us of the stamped launch:", e0.elapsed_time(e1) * 1e3)
 h = np.zeros(8 * 1024, dtype=np.uint64)
 lib.nvl_diag_fstamps.restype = ctypes.c_int
 lib.nvl_diag_fstamps(h.ctypes.data_as(ctypes.c_void_p), h.size)
 h = h.reshape(-1, 8).astype(np.int64)
 h = h[h[:, 0] > 0]
+last = h[h[:, 7] > 0]
+print("last WG end (us after first start):", (last[:, 7] - h[:, 0].min()) / 100.0)
+h[h[:, 7] == 0, 7] = h[h[:, 7] > 0, 7].max() if (h[:, 7] > 0).any() else 0
 t0 = h[:, 0].min()
 us = (h - t0) / 100.0
-for k, name in enumerate(["start", "plan_done", "units_done", "counted", "counts", "runwalk_t0", "scan_sync"]):
+for k, name in enumerate(["start", "plan_done", "units_done", "counted", "counts", "runwalk_t0", "scan_sync", "last_end"]):
     q = np.percentile(us[:, k], [0, 10, 50, 90, 100])
     print(f"{name:11s}", " ".join(f"{x:8.2f}" for x in q))
 print("plan duration p50/max:", np.median(us[:, 1] - us[:, 0]), (us[:, 1] - us[:, 0]).max())

@@ -66,6 +66,54 @@ NVL_API int nvl_sstable_seal_trailers(void* file, uint64_t file_len, const nvl_b
 NVL_API int nvl_sstable_verify_blocks(const void* file, uint64_t file_len, const nvl_block_handle* blocks, size_t n,
                                       uint8_t* verdict, uint64_t* n_bad, uint32_t flags);
 
+/* ---- whole-table verification ------------------------------------------- */
+
+#define NVL_FOOTER_SIZE 48 /* Footer::kEncodedLength, table/format.h:64-66 */
+
+/* table-level outcome of nvl_sstable_verify_table, following Table::Open
+ * (table/table.cc:38-82) and the index block's iterator (table/block.cc) */
+#define NVL_TABLE_OK 0
+#define NVL_TABLE_TOO_SHORT 1       /* "file is too short to be an sstable"  table.cc:44-46 */
+#define NVL_TABLE_BAD_MAGIC 2       /* "not an sstable (bad magic number)"   format.cc:49-51 */
+#define NVL_TABLE_BAD_FOOTER 3      /* "bad block handle" in the footer      format.cc:28-29,54-57 */
+#define NVL_TABLE_INDEX_UNREADABLE 4 /* ReadBlock(index) failed: blocks[0] holds its verdict (table.cc:58-66) */
+#define NVL_TABLE_BAD_INDEX_BLOCK 5 /* "bad block contents" (restart array does not fit, block.cc:26-37,256-259) */
+#define NVL_TABLE_BAD_INDEX_ENTRY 6 /* "bad entry in block": the index scan stopped there (block.cc:218-245);
+                                       the entries before it are listed and verified */
+#define NVL_TABLE_COMPRESSED_INDEX 7 /* index block stored with kSnappyCompression: not parsed here */
+
+/* roles of the blocks nvl_sstable_verify_table lists */
+#define NVL_TBLOCK_INDEX 0
+#define NVL_TBLOCK_METAINDEX 1
+#define NVL_TBLOCK_META 2 /* a block a metaindex entry points at (e.g. "filter.<policy>", table.cc:99-108) */
+#define NVL_TBLOCK_DATA 3
+
+#define NVL_BLOCK_BAD_HANDLE 4 /* the index/metaindex value is not a BlockHandle: "bad block handle"
+                                  (Table::BlockReader table/table.cc:160-165); offset = size = 0 */
+
+typedef struct nvl_table_block {
+  uint64_t offset;
+  uint64_t size;
+  uint32_t role;    /* NVL_TBLOCK_* */
+  uint32_t verdict; /* NVL_BLOCK_* */
+} nvl_table_block;
+
+/* Verify every block of an SSTable image (an mmap'd table file, or its
+ * bytes) with ReadBlock's checks (verify_checksums = true), in ONE batch:
+ * footer -> index block -> every data block handle in index order, plus the
+ * metaindex block and every block its entries point at.  The index and
+ * metaindex blocks are parsed speculatively before their own CRCs are known
+ * so all CRCs go to the GPU together; a block list is only reported from a
+ * parse whose block passed.  Output order: index, metaindex, meta blocks (in
+ * metaindex order; only when the metaindex verified), data blocks (only when
+ * the index verified).  *table_status gets NVL_TABLE_*; *n_blocks the number
+ * of blocks listed (at most `cap` written, NVL_CRC32C_ENOSPC if more; blocks
+ * may be NULL to query); *n_bad (optional) the listed blocks whose verdict is
+ * not OK.  Compressed (type 1) data/meta blocks verify as OK here, as in
+ * nvl_sstable_verify_blocks. */
+NVL_API int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
+                                     size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags);
+
 /* ---- log files ----------------------------------------------------------- */
 
 #define NVL_LOG_BLOCK_SIZE 32768 /* db/log_format.h:27 */

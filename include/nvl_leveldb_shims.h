@@ -336,6 +336,21 @@ inline int VerifyBlocks(const char* file, uint64_t file_len, const std::vector<n
   return nvl_sstable_verify_blocks(file, file_len, blocks.data(), blocks.size(), verdict->data(), n_bad, flags);
 }
 
+// Whole-table verification (Table::Open's footer and index read,
+// table/table.cc:38-82, then ReadBlock with verify_checksums of every block
+// the index and metaindex point at) in one batch: *table_status gets
+// NVL_TABLE_*, blocks the listed blocks with their roles and verdicts.
+inline int VerifyTable(const char* file, uint64_t file_len, std::vector<nvl_table_block>* blocks,
+                       uint32_t* table_status, uint64_t* n_bad, uint32_t flags = 0) {
+  size_t n = 0;
+  int rc = nvl_sstable_verify_table(file, file_len, nullptr, 0, &n, table_status, n_bad, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+  blocks->resize(n);
+  rc = nvl_sstable_verify_table(file, file_len, blocks->data(), n, &n, table_status, n_bad, flags);
+  blocks->resize(rc == NVL_CRC32C_OK ? n : 0);
+  return rc;
+}
+
 }  // namespace shims
 }  // namespace nvl
 

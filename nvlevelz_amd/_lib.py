@@ -57,11 +57,21 @@ SIGNATURES = {
     "nvl_sstable_verify_blocks": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _u32]),
     "nvl_log_scan": (_int, [_vp, _u64, _u64, _int, _vp, _sz, _vp, _u32]),
     "nvl_log_seal": (_int, [_vp, _u64, _vp, _sz, _u32]),
+    "nvl_sstable_verify_table": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _vp, _u32]),
 }
 
 FRAMING_HOST = 0x100
 BLOCK_OK, BLOCK_TRUNCATED, BLOCK_CHECKSUM_MISMATCH, BLOCK_BAD_TYPE = 0, 1, 2, 3
 LOG_RECORD, LOG_BAD_LENGTH, LOG_CHECKSUM, LOG_ZERO, LOG_EOF = 0, 1, 2, 3, 4
+BLOCK_BAD_HANDLE = 4
+(TABLE_OK, TABLE_TOO_SHORT, TABLE_BAD_MAGIC, TABLE_BAD_FOOTER, TABLE_INDEX_UNREADABLE, TABLE_BAD_INDEX_BLOCK,
+ TABLE_BAD_INDEX_ENTRY, TABLE_COMPRESSED_INDEX) = range(8)
+TBLOCK_INDEX, TBLOCK_METAINDEX, TBLOCK_META, TBLOCK_DATA = 0, 1, 2, 3
+
+
+class TableBlock(ctypes.Structure):
+    """nvl_table_block (include/nvl_framing.h)."""
+    _fields_ = [("offset", _u64), ("size", _u64), ("role", _u32), ("verdict", _u32)]
 
 
 class LogEvent(ctypes.Structure):

@@ -59,6 +59,71 @@ struct BlockParse {
   nvl_log_event closing;    // BAD_LENGTH / ZERO / EOF, or kind = UINT32_MAX (none: trailer skipped)
 };
 
+// ---- SSTable structure (whole-table verify) --------------------------------
+
+constexpr uint64_t kTableMagic = 0xdb4775248b80fb57ull;  // table/format.h:77
+
+// GetVarint64Ptr / GetVarint32Ptr (util/coding.cc): at most 10 / 5 bytes, never past limit.
+const uint8_t* get_varint(const uint8_t* p, const uint8_t* limit, unsigned max_shift, uint64_t* v) {
+  uint64_t r = 0;
+  for (unsigned shift = 0; shift <= max_shift && p < limit; shift += 7) {
+    const uint64_t b = *p++;
+    if (b & 128) {
+      r |= (b & 127) << shift;
+    } else {
+      *v = r | (b << shift);
+      return p;
+    }
+  }
+  return nullptr;
+}
+
+// BlockHandle::DecodeFrom (table/format.cc:23-30); trailing bytes are allowed.
+const uint8_t* decode_handle(const uint8_t* p, const uint8_t* limit, nvl_block_handle* h) {
+  p = get_varint(p, limit, 63, &h->offset);
+  return p ? get_varint(p, limit, 63, &h->size) : nullptr;
+}
+
+// The entries of a block as Block::Iter walks them from SeekToFirst
+// (table/block.cc:17-37, 47-72, 219-246): one handle per entry value, an
+// undecodable value recorded as a bad handle.  Returns NVL_TABLE_OK,
+// NVL_TABLE_BAD_INDEX_BLOCK or NVL_TABLE_BAD_INDEX_ENTRY (entries before the
+// bad one are kept, as the iterator yields them).
+uint32_t block_handles(const uint8_t* data, uint64_t size, std::vector<nvl_block_handle>* out,
+                       std::vector<uint8_t>* bad) {
+  if (size < 4) return NVL_TABLE_BAD_INDEX_BLOCK;  // Block::Block size_ = 0 -> "bad block contents"
+  const uint64_t num_restarts = load_le32(data + size - 4);
+  if (num_restarts > (size - 4) / 4) return NVL_TABLE_BAD_INDEX_BLOCK;
+  if (num_restarts == 0) return NVL_TABLE_OK;  // NewEmptyIterator
+  const uint64_t restarts = size - (1 + num_restarts) * 4;
+  const uint8_t* limit = data + restarts;
+  uint64_t cur = load_le32(data + restarts);  // SeekToRestartPoint(0): GetRestartPoint(0)
+  uint64_t key_len = 0;
+  while (cur < restarts) {
+    const uint8_t* p = data + cur;
+    uint64_t shared, non_shared, value_len;
+    if (limit - p < 3) return NVL_TABLE_BAD_INDEX_ENTRY;
+    if ((p[0] | p[1] | p[2]) < 128) {
+      shared = p[0], non_shared = p[1], value_len = p[2];
+      p += 3;
+    } else if (!(p = get_varint(p, limit, 28, &shared)) || !(p = get_varint(p, limit, 28, &non_shared)) ||
+               !(p = get_varint(p, limit, 28, &value_len))) {
+      return NVL_TABLE_BAD_INDEX_ENTRY;
+    }
+    // block.cc:70 (a 64-bit sum: the reference's uint32_t sum could wrap and read past the block)
+    if ((uint64_t)(limit - p) < non_shared + value_len || key_len < shared)
+      return NVL_TABLE_BAD_INDEX_ENTRY;
+    key_len = shared + non_shared;
+    const uint8_t* value = p + non_shared;
+    nvl_block_handle h{0, 0};
+    const bool ok = decode_handle(value, value + value_len, &h) != nullptr;
+    out->push_back(ok ? h : nvl_block_handle{0, 0});
+    bad->push_back(!ok);
+    cur = (uint64_t)(value + value_len - data);
+  }
+  return NVL_TABLE_OK;
+}
+
 }  // namespace
 }  // namespace nvl
 
@@ -236,6 +301,86 @@ int nvl_log_seal(void* data, uint64_t len, const uint64_t* header_offsets, size_
   const int rc = value_many(d, len, off, ln, &crc, flags);
   if (rc != NVL_CRC32C_OK) return rc;
   for (size_t i = 0; i < n; ++i) store_le32(d + header_offsets[i], mask(crc[i]));  // :95-96
+  return NVL_CRC32C_OK;
+}
+
+int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
+                             size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags) {
+  if (n_blocks) *n_blocks = 0;
+  if (n_bad) *n_bad = 0;
+  if ((!file && file_len) || !n_blocks || !table_status) return NVL_CRC32C_EINVAL;
+  const uint8_t* f = static_cast<const uint8_t*>(file);
+  *table_status = NVL_TABLE_OK;
+
+  // Table::Open (table/table.cc:38-55): footer.
+  if (file_len < NVL_FOOTER_SIZE) {
+    *table_status = NVL_TABLE_TOO_SHORT;
+    return NVL_CRC32C_OK;
+  }
+  const uint8_t* footer = f + file_len - NVL_FOOTER_SIZE;
+  const uint64_t magic = (uint64_t)load_le32(footer + 40) | ((uint64_t)load_le32(footer + 44) << 32);
+  if (magic != kTableMagic) {  // format.cc:43-51
+    *table_status = NVL_TABLE_BAD_MAGIC;
+    return NVL_CRC32C_OK;
+  }
+  nvl_block_handle meta_h, index_h;
+  const uint8_t* fp = decode_handle(footer, footer + NVL_FOOTER_SIZE, &meta_h);  // format.cc:53-56
+  if (!fp || !decode_handle(fp, footer + NVL_FOOTER_SIZE, &index_h)) {
+    *table_status = NVL_TABLE_BAD_FOOTER;
+    return NVL_CRC32C_OK;
+  }
+
+  // Speculative parse of the index and metaindex blocks (their CRCs are
+  // checked in the same batch as the blocks they point at).
+  auto contents = [&](const nvl_block_handle& h) { return block_in_file(h, file_len) ? f + h.offset : nullptr; };
+  std::vector<nvl_block_handle> data_h, meta_blocks;
+  std::vector<uint8_t> data_bad, meta_bad;
+  uint32_t index_parse = NVL_TABLE_OK;
+  const uint8_t* index_data = contents(index_h);
+  if (index_data && index_data[index_h.size] == 0)
+    index_parse = block_handles(index_data, index_h.size, &data_h, &data_bad);
+  const uint8_t* meta_data = contents(meta_h);
+  if (meta_data && meta_data[meta_h.size] == 0) block_handles(meta_data, meta_h.size, &meta_blocks, &meta_bad);
+
+  // One CRC batch: index, metaindex, then every decodable in-file handle.
+  std::vector<nvl_block_handle> all;
+  all.reserve(2 + meta_blocks.size() + data_h.size());
+  all.push_back(index_h);
+  all.push_back(meta_h);
+  for (size_t i = 0; i < meta_blocks.size(); ++i) all.push_back(meta_blocks[i]);
+  for (size_t i = 0; i < data_h.size(); ++i) all.push_back(data_h[i]);
+  std::vector<uint8_t> verdict(all.size());
+  const int rc = nvl_sstable_verify_blocks(f, file_len, all.data(), all.size(), verdict.data(), nullptr, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+
+  std::vector<nvl_table_block> out;
+  auto emit = [&](const nvl_block_handle& h, uint32_t role, uint32_t v) {
+    out.push_back(nvl_table_block{h.offset, h.size, role, v});
+  };
+  emit(index_h, NVL_TBLOCK_INDEX, verdict[0]);
+  if (verdict[0] != NVL_BLOCK_OK) {  // Table::Open fails on the index block (table.cc:58-66)
+    *table_status = NVL_TABLE_INDEX_UNREADABLE;
+  } else if (index_data[index_h.size] != 0) {
+    *table_status = NVL_TABLE_COMPRESSED_INDEX;
+  } else {
+    emit(meta_h, NVL_TBLOCK_METAINDEX, verdict[1]);
+    const bool meta_ok = verdict[1] == NVL_BLOCK_OK && meta_data[meta_h.size] == 0;
+    size_t k = 2;
+    for (size_t i = 0; i < meta_blocks.size(); ++i, ++k)
+      if (meta_ok) emit(meta_blocks[i], NVL_TBLOCK_META, meta_bad[i] ? NVL_BLOCK_BAD_HANDLE : verdict[k]);
+    for (size_t i = 0; i < data_h.size(); ++i, ++k)
+      emit(data_h[i], NVL_TBLOCK_DATA, data_bad[i] ? NVL_BLOCK_BAD_HANDLE : verdict[k]);
+    *table_status = index_parse;
+  }
+  *n_blocks = out.size();
+  if (n_bad) {
+    uint64_t b = 0;
+    for (const nvl_table_block& t : out) b += t.verdict != NVL_BLOCK_OK;
+    *n_bad = b;
+  }
+  if (!blocks) return NVL_CRC32C_OK;
+  if (out.size() > cap) return NVL_CRC32C_ENOSPC;
+  if (!out.empty()) memcpy(blocks, out.data(), out.size() * sizeof(nvl_table_block));
   return NVL_CRC32C_OK;
 }
 

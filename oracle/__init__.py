@@ -247,6 +247,8 @@ class _RefFraming:
         lib.ref_log_read.argtypes = [vp, sz, ctypes.c_int, u64, vp, sz, vp]
         lib.ref_read_block.restype = ctypes.c_int
         lib.ref_read_block.argtypes = [vp, sz, u64, u64, ctypes.c_char_p, sz]
+        lib.ref_table_scan.restype = ctypes.c_int
+        lib.ref_table_scan.argtypes = [vp, sz, vp, sz, vp]
         self.lib = lib
 
     def log_write(self, payloads: list[bytes], dest_length: int = 0) -> bytes:
@@ -266,6 +268,14 @@ class _RefFraming:
         n = ctypes.c_size_t(0)
         rc = self.lib.ref_log_read(image or b"\0", len(image), int(checksum), initial_offset, out, cap,
                                    ctypes.byref(n))
+        assert rc == 0, rc
+        return out.raw[:n.value].decode()
+
+    def table_scan(self, image: bytes) -> str:
+        cap = 96 * (len(image) // 3 + 16) + 4096
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        rc = self.lib.ref_table_scan(image or b"\0", len(image), out, cap, ctypes.byref(n))
         assert rc == 0, rc
         return out.raw[:n.value].decode()
 

@@ -206,17 +206,35 @@ def configs(do_cfg4: bool) -> dict:
     return out
 
 
+def table_cases() -> dict:
+    """SSTable scenarios (tests/table_cases.py) scanned by the REFERENCE's own
+    Footer::DecodeFrom, ReadBlock and Block::Iter (table/format.cc,
+    table/block.cc) through oracle/ref_framing.cc:ref_table_scan."""
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN)))
+    import table_cases as tc  # tests/table_cases.py
+    p = oracle.port()
+    rf = oracle.ref_framing()
+    cases = []
+    for spec in tc.named() + tc.random_cases(300):
+        img, _ = tc.build(p, spec)
+        c = dict(spec)
+        c.update({"image_len": len(img), "image_crc": p.value(img), "trace": rf.table_scan(img)})
+        cases.append(c)
+    return {"cases": cases}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-cfg4", action="store_true")
-    ap.add_argument("--only", default="", help="comma list of fixtures to regenerate (kat,sweep,framing,log_cases,configs)")
+    ap.add_argument("--only", default="", help="comma list of fixtures to regenerate (kat,sweep,framing,log_cases,table_cases,configs)")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     os.makedirs(GOLDEN, exist_ok=True)
     provenance = {"generator": "oracle/gen_golden.py",
                   "reference_builds": [oracle.ref("sse").path, oracle.ref("table").path,
                                        os.path.join(os.path.dirname(oracle.ref("sse").path), "libref_framing.so")]}
-    for name, fn in [("kat", kat), ("sweep", sweep), ("framing", framing), ("log_cases", log_cases)]:
+    for name, fn in [("kat", kat), ("sweep", sweep), ("framing", framing), ("log_cases", log_cases),
+                     ("table_cases", table_cases)]:
         if only and name not in only:
             continue
         d = fn()

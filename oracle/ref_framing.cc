@@ -3,7 +3,8 @@
 //
 // TEST INFRASTRUCTURE ONLY.  This file holds no reference code: it includes
 // reference headers from /root/reference and is linked (oracle/Makefile)
-// against db/log_reader.cc, db/log_writer.cc, table/format.cc,
+// against db/log_reader.cc, db/log_writer.cc, table/format.cc, table/block.cc,
+// table/iterator.cc, util/comparator.cc,
 // util/{crc32c,coding,status,env}.cc and port/port_posix_sse.cc compiled
 // straight from /root/reference into oracle/_ref/libref_framing.so.  The
 // in-memory file classes below implement the reference's public interfaces
@@ -21,6 +22,9 @@
 #include "db/log_writer.h"
 #include "leveldb/env.h"
 #include "leveldb/options.h"
+#include "leveldb/comparator.h"
+#include "leveldb/iterator.h"
+#include "table/block.h"
 #include "table/format.h"
 #include "util/crc32c.h"
 
@@ -159,6 +163,88 @@ int ref_read_block(const uint8_t* file, size_t len, uint64_t offset, uint64_t si
   const std::string m = s.ok() ? std::string() : s.ToString();
   snprintf(msg, cap, "%s", m.c_str());
   return s.ok() ? 0 : 1;
+}
+
+// Whole-table verification with the reference's own pieces, in the order
+// Table::Open (table/table.cc:38-82) and its two-level iterator use them:
+// Footer::DecodeFrom, ReadBlock(index, verify_checksums), Block::Iter over the
+// index (BytewiseComparator), BlockHandle::DecodeFrom of every value and
+// ReadBlock of every data block; and the same over the metaindex block and
+// every block its entries point at (ReadMeta, table.cc:84-110, reads the
+// "filter." one).  Trace lines:
+//   "T <Status::ToString()>"            footer / index failure (then nothing else)
+//   "B <role> <offset> <size> <status>" per block (role: 0 index, 1 metaindex, 2 meta, 3 data;
+//                                       status "OK", a ReadBlock status, or the DecodeFrom status)
+//   "S <role> <status>"                 a non-OK block iterator status after the scan
+__attribute__((visibility("default")))
+int ref_table_scan(const uint8_t* file, size_t len, char* trace, size_t cap, size_t* trace_len) {
+  using leveldb::Status;
+  MemRandomAccess f(reinterpret_cast<const char*>(file), len);
+  leveldb::ReadOptions opt;
+  opt.verify_checksums = true;
+  std::string t;
+  char buf[160];
+  auto line = [&](int role, const leveldb::BlockHandle& h, const Status& s) {
+    snprintf(buf, sizeof(buf), "B %d %llu %llu ", role, (unsigned long long)h.offset(),
+             (unsigned long long)h.size());
+    t.append(buf);
+    t.append(s.ok() ? std::string("OK") : s.ToString());
+    t.push_back('\n');
+  };
+  if (len < leveldb::Footer::kEncodedLength) {
+    t = "T " + Status::Corruption("file is too short to be an sstable").ToString() + "\n";
+    return copy_out(t, trace, cap, trace_len);
+  }
+  leveldb::Slice footer_input(reinterpret_cast<const char*>(file) + len - leveldb::Footer::kEncodedLength,
+                              leveldb::Footer::kEncodedLength);
+  leveldb::Footer footer;
+  Status s = footer.DecodeFrom(&footer_input);
+  if (!s.ok()) {
+    t = "T " + s.ToString() + "\n";
+    return copy_out(t, trace, cap, trace_len);
+  }
+  // one block and, when it reads, the blocks its entries point at
+  auto walk = [&](const leveldb::BlockHandle& bh, int role, int child_role) -> bool {
+    leveldb::BlockContents bc;
+    Status rs = leveldb::ReadBlock(&f, opt, bh, &bc);
+    line(role, bh, rs);
+    if (!rs.ok()) return false;
+    {
+      leveldb::Block block(bc);  // owns bc.data when heap_allocated
+      leveldb::Iterator* it = block.NewIterator(leveldb::BytewiseComparator());
+      for (it->SeekToFirst(); it->Valid(); it->Next()) {
+        leveldb::BlockHandle h;
+        leveldb::Slice v = it->value();
+        Status hs = h.DecodeFrom(&v);
+        if (!hs.ok()) {
+          leveldb::BlockHandle z;
+          z.set_offset(0);
+          z.set_size(0);
+          line(child_role, z, hs);
+          continue;
+        }
+        leveldb::BlockContents c;
+        // ReadBlock allocates size + 5 bytes before it reads; a handle larger
+        // than the file cannot be read from it (the Read would come back short)
+        Status cs = h.size() > len ? Status::Corruption("truncated block read") : leveldb::ReadBlock(&f, opt, h, &c);
+        if (cs.ok() && c.heap_allocated) delete[] c.data.data();
+        line(child_role, h, cs);
+      }
+      if (!it->status().ok()) {
+        snprintf(buf, sizeof(buf), "S %d ", role);
+        t.append(buf);
+        t.append(it->status().ToString());
+        t.push_back('\n');
+      }
+      delete it;
+    }
+    return true;
+  };
+  if (!walk(footer.index_handle(), 0, 3)) {
+    return copy_out(t, trace, cap, trace_len);
+  }
+  walk(footer.metaindex_handle(), 1, 2);
+  return copy_out(t, trace, cap, trace_len);
 }
 
 }  // extern "C"

@@ -74,4 +74,24 @@ int shim_log_read(const uint8_t* file, size_t len, int checksum, uint64_t initia
   return copy_out(t, trace, cap, trace_len);
 }
 
+// nvl::shims::VerifyTable over a table image: "<status> <n_bad>" then one
+// "<offset> <size> <role> <verdict>" line per listed block.
+__attribute__((visibility("default")))
+int shim_table_verify(const uint8_t* file, size_t len, uint32_t flags, char* trace, size_t cap, size_t* trace_len) {
+  std::vector<nvl_table_block> blocks;
+  uint32_t status = 0;
+  uint64_t n_bad = 0;
+  const int rc = nvl::shims::VerifyTable(reinterpret_cast<const char*>(file), len, &blocks, &status, &n_bad, flags);
+  if (rc != NVL_CRC32C_OK) return rc;
+  char buf[96];
+  snprintf(buf, sizeof(buf), "%u %llu\n", status, (unsigned long long)n_bad);
+  std::string t(buf);
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    snprintf(buf, sizeof(buf), "%llu %llu %u %u\n", (unsigned long long)blocks[i].offset,
+             (unsigned long long)blocks[i].size, blocks[i].role, blocks[i].verdict);
+    t.append(buf);
+  }
+  return copy_out(t, trace, cap, trace_len);
+}
+
 }  // extern "C"

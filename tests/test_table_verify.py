@@ -1,0 +1,186 @@
+"""Whole-table verification (nvl_sstable_verify_table, include/nvl_framing.h;
+nvl::shims::VerifyTable, include/nvl_leveldb_shims.h): footer -> index block
+-> every data block, plus the metaindex and the blocks it points at, all
+checked with ReadBlock's rules in one CRC batch.
+
+Parity anchors:
+* tests/golden/table_cases.json -- 330 table images (tests/table_cases.py:
+  named cases for every Table::Open / ReadBlock / Block::Iter outcome plus
+  seeded random ones) scanned by the REFERENCE's own Footer::DecodeFrom,
+  ReadBlock and Block::Iter (table/format.cc, table/block.cc, built from
+  /root/reference; oracle/ref_framing.cc:ref_table_scan).  The image is
+  rebuilt from its spec and checked against the stored length and CRC first.
+* live, where oracle/_ref/libref_framing.so exists: 200 further random tables.
+* at size: a 10^5-block table (~400 MB) on the GPU -- every block verifies,
+  then exactly the corrupted ones fail (size-independent property).
+
+Each check runs with NVL_FRAMING_HOST (CPU suite) and on the GPU (marked gpu).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import table_cases as tc
+from conftest import ROOT, gpu_present, load_golden
+
+HOST = 0x100
+NATIVE = os.path.join(ROOT, "tests", "native")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from nvlevelz_amd import _lib
+    return _lib
+
+
+@pytest.fixture(scope="module")
+def harness(L):
+    path = os.path.join(NATIVE, "libshim_harness.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-s", "-C", NATIVE], check=True)
+    lib = ctypes.CDLL(path)
+    vp, sz, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32
+    lib.shim_table_verify.restype = ctypes.c_int
+    lib.shim_table_verify.argtypes = [vp, sz, u32, vp, sz, vp]
+    return lib
+
+
+def verify(L, img: bytes, flags: int):
+    n = ctypes.c_size_t(0)
+    st = ctypes.c_uint32(0)
+    nb = ctypes.c_uint64(0)
+    lib = L.lib
+    assert lib.nvl_sstable_verify_table(img, len(img), None, 0, ctypes.byref(n), ctypes.byref(st),
+                                        ctypes.byref(nb), flags) == 0
+    arr = (L.TableBlock * max(n.value, 1))()
+    assert lib.nvl_sstable_verify_table(img, len(img), arr, n.value, ctypes.byref(n), ctypes.byref(st),
+                                        ctypes.byref(nb), flags) == 0
+    blocks = [(a.offset, a.size, a.role, a.verdict) for a in arr[:n.value]]
+    assert nb.value == sum(b[3] != 0 for b in blocks)
+    return st.value, blocks
+
+
+def via_header(harness, img: bytes, flags: int):
+    cap = 64 * (len(img) // 8 + 16)
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    assert harness.shim_table_verify(img, len(img), flags, out, cap, ctypes.byref(n)) == 0
+    lines = out.raw[:n.value].decode().splitlines()
+    st, _ = map(int, lines[0].split())
+    return st, [tuple(map(int, x.split())) for x in lines[1:]]
+
+
+def _check_golden(L, harness, port, flags):
+    cases = load_golden("table_cases")["cases"]
+    assert len(cases) >= 300
+    for c in cases:
+        img, _ = tc.build(port, c)
+        assert len(img) == c["image_len"] and port.value(img) == c["image_crc"], c["name"]
+        want = tc.expected(c["trace"])
+        assert verify(L, img, flags) == want, c["name"]
+        if c["name"].startswith("random_") and int(c["name"][7:]) % 10:
+            continue
+        assert via_header(harness, img, flags) == want, c["name"]
+
+
+def test_table_cases_golden_host(L, harness, port):
+    _check_golden(L, harness, port, HOST)
+
+
+@pytest.mark.gpu
+def test_table_cases_golden_gpu(L, harness, port):
+    if not gpu_present():
+        pytest.skip("no GPU")
+    _check_golden(L, harness, port, 0)
+
+
+def test_table_cases_vs_reference_live(L, port):
+    import oracle
+    if not oracle.ref_framing_available():
+        pytest.skip("reference build (oracle/_ref) not present")
+    rf = oracle.ref_framing()
+    for spec in tc.random_cases(200, seed=99):
+        img, _ = tc.build(port, spec)
+        assert verify(L, img, HOST) == tc.expected(rf.table_scan(img)), spec["name"]
+
+
+def test_table_verify_arguments(L):
+    lib = L.lib
+    n = ctypes.c_size_t(7)
+    st = ctypes.c_uint32(9)
+    assert lib.nvl_sstable_verify_table(None, 5, None, 0, ctypes.byref(n), ctypes.byref(st), None, HOST) == L.EINVAL
+    assert lib.nvl_sstable_verify_table(b"", 0, None, 0, None, ctypes.byref(st), None, HOST) == L.EINVAL
+    assert lib.nvl_sstable_verify_table(b"", 0, None, 0, ctypes.byref(n), ctypes.byref(st), None, HOST) == 0
+    assert (n.value, st.value) == (0, L.TABLE_TOO_SHORT)
+
+
+def test_table_verify_enospc(L, port):
+    img, _ = tc.build(port, {"seed": 3, "nblocks": 5, "nmeta": 1})
+    n = ctypes.c_size_t(0)
+    st = ctypes.c_uint32(0)
+    arr = (L.TableBlock * 3)()
+    assert L.lib.nvl_sstable_verify_table(img, len(img), arr, 3, ctypes.byref(n), ctypes.byref(st), None,
+                                          HOST) == L.ENOSPC
+    assert n.value == 1 + 1 + 1 + 5
+
+
+def _big_table(port, nblocks: int, block_bytes: int):
+    """A table of nblocks data blocks of ~block_bytes (one key-value entry
+    each), written with numpy: returns (image, data handles)."""
+    ent_hdr = tc.varint(0) + tc.varint(16) + tc.varint(block_bytes - 30)
+    vlen = block_bytes - 30
+    body = len(ent_hdr) + 16 + vlen
+    size = body + 8  # one restart + count
+    stride = size + 5
+    payload = port.fill(77, 0, nblocks * vlen).reshape(nblocks, vlen)
+    img = np.zeros(nblocks * stride, dtype=np.uint8).reshape(nblocks, stride)
+    img[:, :len(ent_hdr)] = np.frombuffer(ent_hdr, dtype=np.uint8)
+    keys = np.array([list(b"k%015d" % i) for i in range(nblocks)], dtype=np.uint8)
+    img[:, len(ent_hdr):len(ent_hdr) + 16] = keys
+    img[:, len(ent_hdr) + 16:body] = payload
+    img[:, body + 4] = 1  # num_restarts = 1 (restart[0] = 0)
+    flat = img.reshape(-1)
+    handles = np.stack([np.arange(nblocks, dtype=np.uint64) * stride, np.full(nblocks, size, np.uint64)], 1)
+    # trailers: type 0 + Mask(Value(block | type)), sealed by the shim on the host
+    buf = bytearray(flat.tobytes())
+    return buf, handles, size
+
+
+@pytest.mark.gpu
+def test_table_verify_large_gpu(L, port):
+    """10^5 data blocks of 4 KiB: all verify; then exactly the corrupted ones fail."""
+    if not gpu_present():
+        pytest.skip("no GPU")
+    nblocks = 100_000
+    buf, handles, size = _big_table(port, nblocks, 4096)
+    h = np.ascontiguousarray(handles)
+    cbuf = (ctypes.c_char * len(buf)).from_buffer(buf)
+    assert L.lib.nvl_sstable_seal_trailers(cbuf, len(buf), h.ctypes.data, nblocks, 0) == 0
+    del cbuf  # release the export so the image can grow
+    data_end = len(buf)
+    w = tc._Writer(port)
+    w.img = buf
+    meta_h = w.raw(tc.block([], 16))
+    index = tc.block([(b"k%015d" % i, tc.handle(int(o), int(s))) for i, (o, s) in enumerate(handles)], 1)
+    index_h = w.raw(index)
+    foot = tc.handle(*meta_h) + tc.handle(*index_h)
+    w.img += foot + bytes(40 - len(foot)) + tc.MAGIC.to_bytes(8, "little")
+    img = bytes(w.img)
+    st, blocks = verify(L, img, 0)
+    assert st == 0 and len(blocks) == nblocks + 2
+    assert all(b[3] == 0 for b in blocks)
+    assert [b[:2] for b in blocks[2:]] == [(int(o), int(s)) for o, s in handles]
+    rng = np.random.default_rng(11)
+    bad_idx = sorted(set(int(x) for x in rng.integers(0, nblocks, 40)))
+    mut = bytearray(img)
+    for k in bad_idx:
+        o = int(handles[k][0])
+        mut[o + int(rng.integers(0, size))] ^= 1 << int(rng.integers(0, 8))
+    assert data_end < len(mut)
+    st, blocks = verify(L, bytes(mut), 0)
+    assert st == 0
+    assert [i for i, b in enumerate(blocks[2:]) if b[3]] == bad_idx
+    assert all(blocks[2 + k][3] == L.BLOCK_CHECKSUM_MISMATCH for k in bad_idx)

@@ -124,12 +124,20 @@ def main():
         if world == 1 and args.gpus > 1:
             print(f"[bench] --gpus {args.gpus} needs torch.distributed.run; running 1 rank", file=sys.stderr)
         args.gpus = world
-    dev = torch.device("cuda", local)
+    # NVL_BENCH_BACKEND=gloo rehearses the N-rank path on fewer GPUs (ranks
+    # share devices round-robin); the default is RCCL with one GPU per rank.
+    backend = os.environ.get("NVL_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % ndev if backend == "gloo" else local)
     torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)  # RCCL; timing/verification only
-    crc32c.init(local)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)  # RCCL; timing/verification only
+    red_dev = torch.device("cpu") if backend == "gloo" else dev
+    crc32c.init(dev.index)
 
     N = world
     if args.config == "cfg2":
@@ -201,10 +209,10 @@ def main():
     torch.cuda.synchronize()
     kern_ms = [kev[2 * k].elapsed_time(kev[2 * k + 1]) for k in range(len(kev) // 2)]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nt = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        nt = torch.tensor([n_local], dtype=torch.int64, device=red_dev)
         dist.all_reduce(nt, op=dist.ReduceOp.SUM)
         total_blocks = int(nt.item())
     else:

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Rehearse bench.py's N-rank path (torch.distributed.run, barrier, max-over-ranks
+# timing, round-robin shards) on a 1-GPU box: ranks share the GPU and meet over
+# gloo (NVL_BENCH_BACKEND=gloo); the 8-GPU node run uses RCCL, one GPU per rank.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd $R
+export NVL_BENCH_BACKEND=gloo
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29531 bench.py --gpus 2 --steps 50 --warmup 10 --no-cpu > $OUT/dist_n2.json 2> $OUT/dist_n2.err
+rc=$?; echo "[dist] n2 rc=$rc"; cat $OUT/dist_n2.json
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+  --master-port 29532 bench.py --gpus 4 --config cfg5 --steps 5 --warmup 2 --no-cpu > $OUT/dist_n4_cfg5.json 2> $OUT/dist_n4_cfg5.err
+rc=$?; echo "[dist] n4 cfg5 rc=$rc"; cat $OUT/dist_n4_cfg5.json
+exit $rc

@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host end to end")
+    ap.add_argument("--shims", action="store_true",
+                    help="also time the whole-table verify shim on a host-resident 10^5-block SSTable image")
     ap.add_argument("--verify", action="store_true", default=True)
     return ap.parse_args()
 
@@ -108,6 +110,121 @@ def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int) -> dict
         "host_cpu": model, "host_nproc": os.cpu_count(),
         "_check": r_all,
     }
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 128:
+        out.append((v & 127) | 128)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def shim_bench(nblocks: int = 100_000) -> dict:
+    """nvl_sstable_verify_table (include/nvl_framing.h) over a host-resident
+    SSTable image of `nblocks` 4 KiB data blocks (table/format.h layout: one
+    key-value entry + restart array per block, 5-byte trailers, an index with
+    one BlockHandle per block, an empty metaindex, the 48-byte footer), as a
+    caller with an mmap'd table would run it: file bytes in host memory ->
+    one staging copy + H2D + batch kernel + D2H of the CRCs.  Beside it, the
+    same walk with the host CRC (NVL_FRAMING_HOST) and, where the reference
+    build exists, the reference's own Footer/ReadBlock/Block::Iter scan
+    (oracle/_ref, single thread) -- the CPU legs are reported baselines."""
+    import ctypes
+    from nvlevelz_amd import _lib
+    L = _lib.lib
+    S = 4096
+    key_len = 16
+    hdr = _varint(0) + _varint(key_len)
+    vlen = S - 8 - key_len - len(hdr) - 2
+    hdr += _varint(vlen)
+    assert len(hdr) + key_len + vlen + 8 == S
+    stride = S + 5
+    rng = np.random.default_rng(2024)
+    img = np.zeros((nblocks, stride), dtype=np.uint8)
+    img[:, :len(hdr)] = np.frombuffer(hdr, dtype=np.uint8)
+    keys = np.frombuffer(b"".join(b"k%015d" % i for i in range(nblocks)), dtype=np.uint8).reshape(nblocks, key_len)
+    img[:, len(hdr):len(hdr) + key_len] = keys
+    img[:, len(hdr) + key_len:S - 8] = rng.integers(0, 256, size=(nblocks, vlen), dtype=np.uint8)
+    img[:, S - 4] = 1  # num_restarts = 1, restart[0] = 0
+    data = bytearray(img.reshape(-1).tobytes())
+    del img
+    handles = np.stack([np.arange(nblocks, dtype=np.uint64) * stride, np.full(nblocks, S, np.uint64)], 1)
+    cbuf = (ctypes.c_char * len(data)).from_buffer(data)
+    rc = L.nvl_sstable_seal_trailers(cbuf, len(data), np.ascontiguousarray(handles).ctypes.data, nblocks, 0)
+    del cbuf
+    assert rc == 0, rc
+
+    def raw_block(contents: bytes) -> tuple:
+        off = len(data)
+        data.extend(contents + b"\0" + bytes(4))
+        h = np.array([[off, len(contents)]], dtype=np.uint64)
+        cb = (ctypes.c_char * len(data)).from_buffer(data)
+        assert L.nvl_sstable_seal_trailers(cb, len(data), h.ctypes.data, 1, _lib.FRAMING_HOST) == 0
+        del cb
+        return off, len(contents)
+
+    meta_h = raw_block((0).to_bytes(4, "little") + (1).to_bytes(4, "little"))
+    parts, restarts, pos = [], [], 0
+    for i in range(nblocks):  # index block, restart interval 1 (table_builder.cc)
+        v = _varint(i * stride) + _varint(S)
+        e = _varint(0) + _varint(key_len) + _varint(len(v)) + (b"k%015d" % i) + v
+        restarts.append(pos)
+        pos += len(e)
+        parts.append(e)
+    index = b"".join(parts) + np.array(restarts, dtype="<u4").tobytes() + len(restarts).to_bytes(4, "little")
+    index_h = raw_block(index)
+    foot = _varint(meta_h[0]) + _varint(meta_h[1]) + _varint(index_h[0]) + _varint(index_h[1])
+    data.extend(foot + bytes(40 - len(foot)) + (0xDB4775248B80FB57).to_bytes(8, "little"))
+    image = bytes(data)
+    del data
+    nbytes = len(image)
+
+    cap = nblocks + 2
+    arr = (_lib.TableBlock * cap)()
+    n = ctypes.c_size_t(0)
+    st = ctypes.c_uint32(0)
+    nb = ctypes.c_uint64(0)
+
+    def run(flags):
+        rc = L.nvl_sstable_verify_table(image, nbytes, arr, cap, ctypes.byref(n), ctypes.byref(st), ctypes.byref(nb),
+                                        flags)
+        assert rc == 0 and st.value == 0 and n.value == cap and nb.value == 0, (rc, st.value, n.value, nb.value)
+
+    def timed(fn, reps):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    t_gpu = timed(lambda: run(0), 7)
+    t_host = timed(lambda: run(_lib.FRAMING_HOST), 3)
+    res = {"what": "nvl_sstable_verify_table on a host-resident table image (footer -> index -> every block), "
+                   "wall clock per call, median",
+           "table": {"data_blocks": nblocks, "block_bytes": S, "file_bytes": nbytes},
+           "gpu": {"ms": round(t_gpu * 1e3, 3), "GiB/s": round(nbytes / t_gpu / 2**30, 3),
+                   "path": "host image -> pinned staging -> H2D -> one batch kernel -> D2H"},
+           "host_crc": {"ms": round(t_host * 1e3, 3), "GiB/s": round(nbytes / t_host / 2**30, 3), "cores": 1,
+                        "path": "same walk, NVL_FRAMING_HOST"}}
+    try:
+        import oracle
+        if oracle.ref_framing_available():
+            rf = oracle.ref_framing()
+            need = len(rf.table_scan(image)) + 1  # sizes the trace buffer once
+            tr = []
+            t_ref = timed(lambda: tr.append(rf.table_scan(image, need)), 3)
+            ok = tr[-1].count(" OK\n") == cap
+            res["cpu_reference"] = {"ms": round(t_ref * 1e3, 3), "GiB/s": round(nbytes / t_ref / 2**30, 3),
+                                    "cores": 1, "all_blocks_ok": ok,
+                                    "path": "reference Footer::DecodeFrom + ReadBlock(verify_checksums) + "
+                                            "Block::Iter over index and metaindex (oracle/_ref, SSE4.2 crc32c)"}
+    except Exception as e:  # the CPU leg is a reported baseline only
+        res["cpu_reference"] = {"error": repr(e)}
+    return res
 
 
 def main():
@@ -284,6 +401,8 @@ def main():
         }
         if e2e:
             line["e2e"] = e2e
+        if args.shims and N == 1:
+            line["shims"] = shim_bench()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

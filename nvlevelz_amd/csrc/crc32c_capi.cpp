@@ -8,8 +8,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -478,6 +480,39 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   return rc;
 }
 
+// Copy src[0, bytes) to dst (device) through the pinned staging buffer hst,
+// slice by slice: workers fill hst slices in order while this thread queues
+// each finished slice's H2D on st.  Returns the first HIP error.
+static hipError_t stage_h2d(uint8_t* dst, uint8_t* hst, const uint8_t* src, uint64_t bytes, hipStream_t st) {
+  constexpr uint64_t kSlice = 8ull << 20;
+  const uint64_t ns = (bytes + kSlice - 1) / kSlice;
+  if (ns <= 1) {
+    memcpy(hst, src, bytes);
+    return bytes ? hipMemcpyAsync(dst, hst, bytes, hipMemcpyHostToDevice, st) : hipSuccess;
+  }
+  const unsigned nw = bytes >= (64ull << 20) ? 4u : 1u;
+  std::vector<std::atomic<uint8_t>> done(ns);
+  for (auto& f : done) f.store(0, std::memory_order_relaxed);
+  std::atomic<uint64_t> next{0};
+  auto work = [&] {
+    for (uint64_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < ns;) {
+      const uint64_t o = k * kSlice, m = std::min(kSlice, bytes - o);
+      memcpy(hst + o, src + o, m);
+      done[k].store(1, std::memory_order_release);
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned w = 0; w < nw; ++w) th.emplace_back(work);
+  hipError_t e = hipSuccess;
+  for (uint64_t k = 0; k < ns; ++k) {
+    while (!done[k].load(std::memory_order_acquire)) std::this_thread::yield();
+    const uint64_t o = k * kSlice, m = std::min(kSlice, bytes - o);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst + o, hst + o, m, hipMemcpyHostToDevice, st);
+  }
+  for (auto& t : th) t.join();
+  return e;
+}
+
 int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const uint64_t* offsets,
                                  const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
                                  uint64_t n, uint32_t flags) {
@@ -498,15 +533,6 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
   uint8_t* hst = static_cast<uint8_t*>(t_staging.get(total));
   if (!hst) return NVL_CRC32C_EHIP;
-  memcpy(hst, static_cast<const uint8_t*>(region) + lo, wbytes);
-  uint64_t* hoff = reinterpret_cast<uint64_t*>(hst + meta_off);
-  uint64_t* hlen = hoff + n;
-  uint32_t* hini = reinterpret_cast<uint32_t*>(hlen + n);
-  for (uint64_t i = 0; i < n; ++i) {
-    hoff[i] = offsets[i] - lo;
-    hlen[i] = lengths[i];
-    hini[i] = init ? init[i] : init_all;
-  }
   hipStream_t st = thread_stream(s->device);
   if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
@@ -516,7 +542,19 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
   void* dws = d + align_up(total, 256) + align_up(n * 4, 256);
-  hipError_t e = hipMemcpyAsync(d, hst, total, hipMemcpyHostToDevice, st);
+  // The window goes to the GPU in slices: the staging copy of slice k+1 (a
+  // few host threads for large windows) overlaps the H2D DMA of slice k, so
+  // the call costs max(copy, PCIe) instead of their sum.
+  hipError_t e = stage_h2d(d, hst, static_cast<const uint8_t*>(region) + lo, wbytes, st);
+  uint64_t* hoff = reinterpret_cast<uint64_t*>(hst + meta_off);
+  uint64_t* hlen = hoff + n;
+  uint32_t* hini = reinterpret_cast<uint32_t*>(hlen + n);
+  for (uint64_t i = 0; i < n; ++i) {
+    hoff[i] = offsets[i] - lo;
+    hlen[i] = lengths[i];
+    hini[i] = init ? init[i] : init_all;
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(d + meta_off, hst + meta_off, total - meta_off, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);

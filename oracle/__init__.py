@@ -271,13 +271,17 @@ class _RefFraming:
         assert rc == 0, rc
         return out.raw[:n.value].decode()
 
-    def table_scan(self, image: bytes) -> str:
-        cap = 96 * (len(image) // 3 + 16) + 4096
-        out = ctypes.create_string_buffer(cap)
+    def table_scan(self, image: bytes, cap: int = 1 << 20) -> str:
+        """ref_table_scan trace; retried once with the exact size when `cap` is short."""
         n = ctypes.c_size_t(0)
-        rc = self.lib.ref_table_scan(image or b"\0", len(image), out, cap, ctypes.byref(n))
-        assert rc == 0, rc
-        return out.raw[:n.value].decode()
+        while True:
+            out = ctypes.create_string_buffer(cap)
+            rc = self.lib.ref_table_scan(image or b"\0", len(image), out, cap, ctypes.byref(n))
+            if rc == -5 and n.value > cap:
+                cap = n.value
+                continue
+            assert rc == 0, rc
+            return out.raw[:n.value].decode()
 
     def read_block(self, image: bytes, offset: int, size: int) -> str:
         msg = ctypes.create_string_buffer(256)

@@ -256,3 +256,25 @@ def test_device_mode_fails_loudly_without_gpu(L):
     log = bytes(7)
     log = b"\x01\x02\x03\x04\x01\x00\x01x"
     assert L.lib.nvl_log_scan(log, len(log), 0, 1, None, 0, ctypes.byref(n), 0) in (L.ENODEV, L.EHIP)
+
+
+def test_python_view_log(port):
+    """nvlevelz_amd.framing.log_seal / log_scan (host CRC): sealed headers match
+    the reference's Mask(Value(type | payload)), a flipped payload byte is a
+    checksum event that drops the rest of its block (log_reader.cc:254-267)."""
+    from nvlevelz_amd import framing
+    img, hdrs = bytearray(), []
+    for k, n in enumerate([10, 300, 0, 5000]):
+        hdrs.append(len(img))
+        img += bytes(4) + bytes([n & 0xFF, n >> 8, 1]) + port.fill(k, 0, n).tobytes()
+    framing.log_seal(img, hdrs, host=True)
+    for h in hdrs:
+        n = img[h + 4] | (img[h + 5] << 8)
+        assert int.from_bytes(img[h:h + 4], "little") == port.mask(port.value(bytes(img[h + 6:h + 7 + n])))
+    ev = framing.log_scan(bytes(img), host=True)
+    assert [e[0] for e in ev] == ["record"] * 4 + ["eof"]
+    assert [e[1] for e in ev[:4]] == hdrs
+    bad = bytearray(img)
+    bad[hdrs[1] + 9] ^= 1
+    ev = framing.log_scan(bytes(bad), host=True)
+    assert [e[0] for e in ev] == ["record", "checksum mismatch", "eof"]

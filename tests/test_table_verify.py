@@ -184,3 +184,43 @@ def test_table_verify_large_gpu(L, port):
     assert st == 0
     assert [i for i, b in enumerate(blocks[2:]) if b[3]] == bad_idx
     assert all(blocks[2 + k][3] == L.BLOCK_CHECKSUM_MISMATCH for k in bad_idx)
+
+
+# ---- Python view (nvlevelz_amd/framing.py) ---------------------------------
+
+def _check_python_view(port, host):
+    from nvlevelz_amd import framing
+    for c in load_golden("table_cases")["cases"][:40]:
+        img, _ = tc.build(port, c)
+        st, want = tc.expected(c["trace"])
+        rep = framing.verify_table(img, host=host)
+        assert rep.status == st, c["name"]
+        assert [(b.offset, b.size, b.verdict) for b in rep.blocks] == [w[:2] + (w[3],) for w in want], c["name"]
+        if st == 0:
+            assert rep.ok == all(w[3] == 0 for w in want)
+        # the same blocks through verify_blocks
+        if rep.blocks:
+            v = framing.verify_blocks(img, [(b.offset, b.size) for b in rep.blocks if b.verdict != 4], host=host)
+            assert list(v) == [b.verdict for b in rep.blocks if b.verdict != 4], c["name"]
+    # a reference-derived status text
+    img, _ = tc.build(port, {"seed": 5, "nblocks": 3, "nmeta": 1, "muts": [["magic"]]})
+    assert framing.verify_table(img, host=host).status_text == "Corruption: not an sstable (bad magic number)"
+
+
+def test_python_view_host(port):
+    _check_python_view(port, True)
+
+
+@pytest.mark.gpu
+def test_python_view_gpu(port):
+    if not gpu_present():
+        pytest.skip("no GPU")
+    _check_python_view(port, False)
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
+def test_python_view_fails_loudly_without_gpu(port):
+    from nvlevelz_amd import framing
+    img, _ = tc.build(port, {"seed": 5, "nblocks": 3, "nmeta": 1})
+    with pytest.raises(framing.FramingError):
+        framing.verify_table(img)

@@ -335,6 +335,45 @@ struct Staging {
 };
 thread_local Staging t_staging;
 
+// Per-thread double-buffered device slabs + streams of nvl_crc32c_fixed_host,
+// kept across calls (a hipMalloc of two 64 MiB slabs, a hipFree that
+// synchronises the device and two stream creations per call were part of
+// every host-resident call's latency).  Rebuilt when the device, the
+// engine generation (nvl_crc32c_shutdown) or the needed size changes; held
+// until then (no destructor: at thread or process exit the HIP runtime may
+// already be torn down, and the process's device memory goes with it).
+struct HostPipe {
+  int device = -1;
+  uint64_t gen = 0;
+  hipStream_t st[2] = {nullptr, nullptr};
+  uint8_t* buf[2] = {nullptr, nullptr};
+  size_t cap = 0;
+  void release() {
+    for (int k = 0; k < 2; ++k) {
+      if (st[k]) (void)hipStreamSynchronize(st[k]);
+      if (buf[k]) (void)hipFree(buf[k]);
+      if (st[k]) (void)hipStreamDestroy(st[k]);
+      buf[k] = nullptr;
+      st[k] = nullptr;
+    }
+    cap = 0;
+  }
+  bool get(int dev, size_t bytes) {
+    const uint64_t g = g_generation.load(std::memory_order_acquire);
+    if (dev == device && g == gen && bytes <= cap && st[0]) return true;
+    release();  // nvl_crc32c_shutdown does not reset the device: the old slabs and streams are still valid
+    device = dev;
+    gen = g;
+    for (int k = 0; k < 2; ++k) {
+      if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) return false;
+      if (hipMalloc(&buf[k], bytes) != hipSuccess) return false;
+    }
+    cap = bytes;
+    return true;
+  }
+};
+thread_local HostPipe t_pipe;
+
 }  // namespace
 }  // namespace nvl
 
@@ -580,19 +619,19 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
   per = std::min<uint64_t>(per, n);
   const uint64_t slab_bytes = (per - 1) * stride + len;
   const size_t ws = fixed_ws_bytes(len, per, s->num_cu);
-  hipStream_t st[2];
-  uint8_t* dbuf[2] = {nullptr, nullptr};
+  if (!t_pipe.get(s->device, align_up(slab_bytes, 256) + per * 8 + ws + 512)) {
+    t_pipe.release();
+    return NVL_CRC32C_EHIP;
+  }
+  hipStream_t* st = t_pipe.st;
+  uint8_t* dbuf[2] = {t_pipe.buf[0], t_pipe.buf[1]};
   uint32_t* dout[2] = {nullptr, nullptr};
   uint32_t* dini[2] = {nullptr, nullptr};
   void* dws[2] = {nullptr, nullptr};
   for (int k = 0; k < 2; ++k) {
-    if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) return NVL_CRC32C_EHIP;
-    if (hipMalloc(&dbuf[k], align_up(slab_bytes, 256) + per * 8 + ws + 512) != hipSuccess) rc = NVL_CRC32C_EHIP;
-    else {
-      dout[k] = reinterpret_cast<uint32_t*>(dbuf[k] + align_up(slab_bytes, 256));
-      dini[k] = dout[k] + per;
-      dws[k] = reinterpret_cast<uint8_t*>(dini[k] + per) + 256 - ((uintptr_t)(dini[k] + per) & 255);
-    }
+    dout[k] = reinterpret_cast<uint32_t*>(dbuf[k] + align_up(slab_bytes, 256));
+    dini[k] = dout[k] + per;
+    dws[k] = reinterpret_cast<uint8_t*>(dini[k] + per) + 256 - ((uintptr_t)(dini[k] + per) & 255);
   }
   const uint8_t* hb = static_cast<const uint8_t*>(base);
   for (uint64_t i0 = 0, k = 0; rc == NVL_CRC32C_OK && i0 < n; i0 += per, k ^= 1) {
@@ -605,11 +644,8 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
                   st[k]);
     if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out + i0, dout[k], m * 4, hipMemcpyDeviceToHost, st[k]));
   }
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 2; ++k)
     if (hipStreamSynchronize(st[k]) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
-    if (dbuf[k]) (void)hipFree(dbuf[k]);
-    (void)hipStreamDestroy(st[k]);
-  }
   return rc;
 }
 

@@ -281,6 +281,38 @@ def test_host_entry_points(dev, C, port):
     assert np.array_equal(got, port.fixed(host, 4096, 4096, 3000))
 
 
+def test_region_host_sliced_staging(dev, C, port):
+    """nvl_crc32c_batch_region_host over a ~75 MB window that starts at a
+    non-zero offset and is not a multiple of the 8 MiB staging slice (the
+    4-thread sliced copy + per-slice H2D path), every CRC against the oracle."""
+    import ctypes
+    from nvlevelz_amd import _lib
+    region = port.fill(0x77, 0, 80_000_000)
+    rng = np.random.default_rng(21)
+    n = 3000
+    lo, hi = 1_234_567, 76_543_211
+    lens = rng.integers(0, 70_000, size=n).astype(np.uint64)
+    offs = (lo + (rng.random(n) * (hi - lo - lens)).astype(np.uint64)).astype(np.uint64)
+    offs[0], lens[0] = lo, 5
+    offs[1], lens[1] = hi - 17, 17
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    out = np.zeros(n, dtype=np.uint32)
+    rc = _lib.lib.nvl_crc32c_batch_region_host(region.ctypes.data, region.nbytes, offs.ctypes.data, lens.ctypes.data,
+                                               inits.ctypes.data, 0, out.ctypes.data, n, 0)
+    assert rc == 0, rc
+    want = [port.extend(int(i), region[int(o):int(o) + int(m)].tobytes()) for i, o, m in zip(inits, offs, lens)]
+    assert [int(x) for x in out] == want
+
+
+def test_fixed_host_pipe_reuse(dev, C, port):
+    """nvl_crc32c_fixed_host keeps its slabs per thread: calls of growing and
+    shrinking size (slab regrow, then reuse) all match the oracle."""
+    for n, L, seed in [(3000, 4096, 1), (40000, 1024, 2), (700, 2 * 4096 + 3, 3), (3000, 4096, 4)]:
+        host = port.fill(seed, 0, n * L)
+        got = C.extend_fixed_host(host, L, L, n)
+        assert np.array_equal(got, port.fixed(host, L, L, n)), (n, L)
+
+
 def test_workspace_contract(dev, C):
     from nvlevelz_amd._lib import Crc32cError, ENOSPC
     n, L = 10, 3 * 4096

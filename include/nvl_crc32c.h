@@ -14,8 +14,14 @@
  *
  * Threading: every entry point is reentrant and thread-safe.  Device
  * entry points are asynchronous on the HIP stream passed in `stream`
- * (a hipStream_t; NULL = the null stream); inputs must stay valid and
+ * (a hipStream_t; NULL = the null stream) and run on THAT stream's device
+ * (the null stream: the caller's current device), whatever the calling
+ * thread's current device is; inputs must stay valid and
  * unmodified and outputs must not be read until that stream is synchronised.
+ * The host-resident entry points run on the caller's current device; one
+ * thread may drive every device in turn (hipSetDevice between calls).  The
+ * streams and staging memory a thread acquires for them are freed when the
+ * thread exits, or by nvl_crc32c_shutdown.
  * The library owns only its lookup tables (one small copy per device,
  * created on first use or by nvl_crc32c_init) and, when the caller passes no
  * workspace, stream-ordered scratch allocated and freed on `stream`.
@@ -107,6 +113,17 @@ NVL_API int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len
                          const uint32_t* init, uint32_t init_all, uint32_t* out,
                          uint32_t flags, void* workspace, size_t workspace_bytes,
                          void* stream);
+
+/* Measurement form of nvl_crc32c_fixed_dev (same arguments and results)
+ * for benchmark harnesses: the call's first kernel dispatch records
+ * `start_event` and its last records `stop_event` (hipEvent_t, either may be
+ * NULL) through hipExtLaunchKernel, so hipEventElapsedTime gives the kernels'
+ * own duration -- what rocprofv3's kernel trace reports -- with no marker
+ * packet between back-to-back launches.  Not needed by the call sites. */
+NVL_API int nvl_crc32c_fixed_dev_timed(const void* base, uint64_t stride, uint64_t len, uint64_t n,
+                                       const uint32_t* init, uint32_t init_all, uint32_t* out,
+                                       uint32_t flags, void* workspace, size_t workspace_bytes,
+                                       void* stream, void* start_event, void* stop_event);
 
 /* Workspace bytes nvl_crc32c_fixed_dev needs for this shape (0 when none). */
 NVL_API size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, uint64_t n);

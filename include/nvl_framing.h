@@ -107,10 +107,12 @@ typedef struct nvl_table_block {
  * parse whose block passed.  Output order: index, metaindex, meta blocks (in
  * metaindex order; only when the metaindex verified), data blocks (only when
  * the index verified).  *table_status gets NVL_TABLE_*; *n_blocks the number
- * of blocks listed (at most `cap` written, NVL_CRC32C_ENOSPC if more; blocks
- * may be NULL to query); *n_bad (optional) the listed blocks whose verdict is
- * not OK.  Compressed (type 1) data/meta blocks verify as OK here, as in
- * nvl_sstable_verify_blocks. */
+ * of blocks listed (at most `cap` written, NVL_CRC32C_ENOSPC if more);
+ * *n_bad (optional) the listed blocks whose verdict is not OK.  `blocks` may
+ * be NULL to query the list's length cheaply: only the footer, the index and
+ * metaindex blocks are read and checked (host CRC, no batch); *n_blocks and
+ * *table_status are then exact and *n_bad is left 0.  Compressed (type 1)
+ * data/meta blocks verify as OK here, as in nvl_sstable_verify_blocks. */
 NVL_API int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
                                      size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags);
 

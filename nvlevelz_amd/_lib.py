@@ -45,6 +45,7 @@ SIGNATURES = {
     "nvl_crc32c_mask": (_u32, [_u32]),
     "nvl_crc32c_unmask": (_u32, [_u32]),
     "nvl_crc32c_fixed_dev": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _u32, _vp, _sz, _vp]),
+    "nvl_crc32c_fixed_dev_timed": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _vp, _vp]),
     "nvl_crc32c_fixed_workspace_bytes": (_sz, [_u64, _u64, _u64]),
     "nvl_crc32c_batch_dev": (_int, [_vp, _vp, _vp, _vp, _u32, _vp, _u64, _u32, _vp, _sz, _vp]),
     "nvl_crc32c_batch_workspace_bytes": (_sz, [_u64]),

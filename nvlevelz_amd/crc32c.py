@@ -85,7 +85,9 @@ def _stream_handle(t) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def _require_dev(t, name: str, dtype=None):
+def _require_dev(t, name: str, dtype=None, device=None):
+    """A contiguous HIP tensor of an allowed dtype, on `device` when given
+    (every operand of a batch lives on the device of the launch stream)."""
     torch = _torch()
     if not isinstance(t, torch.Tensor) or not t.is_cuda:
         raise TypeError(f"{name} must be a CUDA(HIP) tensor")
@@ -93,6 +95,8 @@ def _require_dev(t, name: str, dtype=None):
         raise ValueError(f"{name} must be contiguous")
     if dtype is not None and t.dtype not in dtype:
         raise TypeError(f"{name} has dtype {t.dtype}, expected one of {dtype}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, the batch on {device}")
 
 
 def fixed_workspace_bytes(stride: int, length: int, n: int) -> int:
@@ -119,14 +123,14 @@ def extend_fixed(buf, stride: int, length: int, n: int, init=0, *, mask: bool = 
         raise ValueError("batch extends past the end of buf")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=buf.device)
-    _require_dev(out, "out", (torch.int32, torch.uint32))
+    _require_dev(out, "out", (torch.int32, torch.uint32), buf.device)
     if out.numel() < n:
         raise ValueError("out too small")
     init_ptr, init_all = None, 0
     if isinstance(init, int):
         init_all = init & 0xFFFFFFFF
     else:
-        _require_dev(init, "init", (torch.int32, torch.uint32))
+        _require_dev(init, "init", (torch.int32, torch.uint32), buf.device)
         if init.numel() < n:
             raise ValueError("init too small")
         init_ptr = init.data_ptr()
@@ -157,7 +161,7 @@ class FixedBatch:
             raise ValueError("batch extends past the end of buf")
         self.buf = buf
         self.out = out if out is not None else torch.empty(n, dtype=torch.int32, device=buf.device)
-        _require_dev(self.out, "out", (torch.int32, torch.uint32))
+        _require_dev(self.out, "out", (torch.int32, torch.uint32), buf.device)
         if self.out.numel() < n:
             raise ValueError("out too small")
         self.init = init
@@ -165,7 +169,7 @@ class FixedBatch:
         if isinstance(init, int):
             init_all = init & 0xFFFFFFFF
         else:
-            _require_dev(init, "init", (torch.int32, torch.uint32))
+            _require_dev(init, "init", (torch.int32, torch.uint32), buf.device)
             if init.numel() < n:
                 raise ValueError("init too small")
             init_ptr = init.data_ptr()
@@ -178,6 +182,8 @@ class FixedBatch:
             ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
         if stream is None:
             stream = torch.cuda.current_stream(buf.device)
+        if stream.device != buf.device:
+            raise ValueError(f"stream is on {stream.device}, buf on {buf.device}")
         self.stream = stream
         self._args = (buf.data_ptr() + base_offset, stride, length, n, init_ptr, init_all,
                       self.out.data_ptr(), FLAG_MASK if mask else 0, ws_ptr, ws_bytes, stream.cuda_stream)
@@ -189,6 +195,17 @@ class FixedBatch:
             check(rc, "nvl_crc32c_fixed_dev")
         return self.out
 
+    def launch_timed(self, start, stop):
+        """:meth:`launch` through nvl_crc32c_fixed_dev_timed: the kernel
+        dispatch itself records ``start``/``stop`` (torch.cuda.Event with
+        timing, already materialised by one ``record()``), so their elapsed
+        time is the kernel's own duration and nothing is enqueued between
+        back-to-back launches."""
+        rc = lib.nvl_crc32c_fixed_dev_timed(*self._args, start.cuda_event, stop.cuda_event)
+        if rc:
+            check(rc, "nvl_crc32c_fixed_dev_timed")
+        return self.out
+
 
 def extend_batch(buf, offsets, lengths, init=0, *, mask: bool = False, out=None, workspace=None):
     """out[i] = Extend(init_i, buf[offsets[i] : offsets[i] + lengths[i]]).
@@ -198,22 +215,27 @@ def extend_batch(buf, offsets, lengths, init=0, *, mask: bool = False, out=None,
     """
     torch = _torch()
     _require_dev(buf, "buf", (torch.uint8, torch.int8))
-    _require_dev(offsets, "offsets", (torch.int64, torch.uint64))
-    _require_dev(lengths, "lengths", (torch.int64, torch.uint64))
+    _require_dev(offsets, "offsets", (torch.int64, torch.uint64), buf.device)
+    _require_dev(lengths, "lengths", (torch.int64, torch.uint64), buf.device)
     n = offsets.numel()
     if lengths.numel() != n:
         raise ValueError("offsets and lengths differ in size")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=buf.device)
-    _require_dev(out, "out", (torch.int32, torch.uint32))
+    _require_dev(out, "out", (torch.int32, torch.uint32), buf.device)
+    if out.numel() < n:
+        raise ValueError("out too small")  # the kernel writes n results
     init_ptr, init_all = None, 0
     if isinstance(init, int):
         init_all = init & 0xFFFFFFFF
     else:
-        _require_dev(init, "init", (torch.int32, torch.uint32))
+        _require_dev(init, "init", (torch.int32, torch.uint32), buf.device)
+        if init.numel() < n:
+            raise ValueError("init too small")  # the kernel reads n values
         init_ptr = init.data_ptr()
     ws_ptr, ws_bytes = None, 0
     if workspace is not None:
+        _require_dev(workspace, "workspace", None, buf.device)
         ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
     rc = lib.nvl_crc32c_batch_dev(buf.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), init_ptr, init_all,
                                   out.data_ptr(), n, FLAG_MASK if mask else 0, ws_ptr, ws_bytes,

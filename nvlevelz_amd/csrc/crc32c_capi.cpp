@@ -90,27 +90,36 @@ uint32_t* counters_for(DeviceState* s, hipStream_t st) {
   return c;
 }
 
-// One non-blocking stream per calling thread for the host-resident entry
-// points (a stream per call would also mean a counter block per call).
-hipStream_t thread_stream(int device) {
-  struct TS {
-    int device = -1;
-    hipStream_t st = nullptr;
-  };
-  thread_local TS ts[4];
-  for (auto& t : ts)
-    if (t.st && t.device == device) return t.st;
-  for (auto& t : ts) {
-    if (!t.st) {
-      if (hipStreamCreateWithFlags(&t.st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-      t.device = device;
-      return t.st;
-    }
-  }
-  return nullptr;
+// Drop the counter block of a stream that is about to be destroyed (a later
+// stream may get the same handle value; the block is re-created zeroed).
+void forget_counter(int device, hipStream_t st) {
+  if (device < 0 || device >= kMaxDevices) return;
+  DeviceState* s = g_state[device].load(std::memory_order_acquire);
+  if (!s) return;
+  std::lock_guard<std::mutex> lk(s->cmu);
+  auto it = s->counters.find(st);
+  if (it == s->counters.end()) return;
+  (void)hipFree(it->second);
+  s->counters.erase(it);
 }
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// The device a stream belongs to (the null stream: the calling thread's
+// current device).  Batch calls take their tables and self-test state from
+// it, so a stream of device d always runs with device d's tables whatever
+// the thread's current device is.
+int stream_device(hipStream_t st, int* dev) {
+  if (st) {
+    hipDevice_t d = -1;
+    if (hipStreamGetDevice(st, &d) == hipSuccess && d >= 0) {
+      *dev = d;
+      return NVL_CRC32C_OK;
+    }
+  }
+  if (hipGetDevice(dev) != hipSuccess || *dev < 0) return NVL_CRC32C_ENODEV;
+  return NVL_CRC32C_OK;
+}
 
 int run_self_test(DeviceState* s);
 
@@ -184,7 +193,8 @@ size_t fixed_ws_bytes(uint64_t len, uint64_t n, int num_cu) { return fixed_recs_
 int hip_rc(hipError_t e) { return e == hipSuccess ? NVL_CRC32C_OK : NVL_CRC32C_EHIP; }
 
 int do_fixed(DeviceState* s, const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
-             uint32_t init_all, uint32_t* out, uint32_t flags, void* ws, size_t ws_bytes, hipStream_t st) {
+             uint32_t init_all, uint32_t* out, uint32_t flags, void* ws, size_t ws_bytes, hipStream_t st,
+             hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr) {
   if (n == 0) return NVL_CRC32C_OK;
   if (!out || (!base && len)) return NVL_CRC32C_EINVAL;
   if (n > (1ull << 40) || len > (1ull << 40) || (n > 1 && stride > (1ull << 50))) return NVL_CRC32C_EINVAL;
@@ -196,7 +206,7 @@ int do_fixed(DeviceState* s, const void* base, uint64_t stride, uint64_t len, ui
   } else if (need && ws_bytes < need) {
     return NVL_CRC32C_ENOSPC;
   }
-  LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
+  LaunchCtx lc{st, s->num_cu, s->tables, nullptr, ev_start, ev_stop};
   hipError_t e = launch_fixed(lc, static_cast<const uint8_t*>(base), stride, len, n, init, init_all, out, flags,
                               static_cast<Rec*>(ws));
   if (own) (void)hipFreeAsync(ws, st);
@@ -302,9 +312,12 @@ int run_self_test(DeviceState* s) {
           fprintf(stderr, "[nvl_crc32c] self-test case %zu: gpu 0x%08x want 0x%08x\n", k, ho[k], want[k]);
         }
       }
-      // Debug escape hatch for kernel development only: report but do not disable.
+#if defined(NVL_DEV_TUNING)
+      // Kernel-development builds only (-DNVL_DEV_TUNING, never the shipped
+      // library): report but do not disable.
       const char* skip = getenv("NVL_CRC32C_SELFTEST_REPORT_ONLY");
       if (rc == NVL_CRC32C_ESELFTEST && skip && skip[0] == '1') rc = NVL_CRC32C_OK;
+#endif
     }
   }
   if (d) (void)hipFree(d);
@@ -319,8 +332,10 @@ int run_self_test(DeviceState* s) {
 struct Staging {
   void* host = nullptr;
   size_t host_bytes = 0;
-  ~Staging() {
+  void release() {
     if (host) (void)hipHostFree(host);
+    host = nullptr;
+    host_bytes = 0;
   }
   void* get(size_t bytes) {
     if (bytes > host_bytes) {
@@ -333,15 +348,11 @@ struct Staging {
     return host;
   }
 };
-thread_local Staging t_staging;
-
 // Per-thread double-buffered device slabs + streams of nvl_crc32c_fixed_host,
 // kept across calls (a hipMalloc of two 64 MiB slabs, a hipFree that
 // synchronises the device and two stream creations per call were part of
 // every host-resident call's latency).  Rebuilt when the device, the
-// engine generation (nvl_crc32c_shutdown) or the needed size changes; held
-// until then (no destructor: at thread or process exit the HIP runtime may
-// already be torn down, and the process's device memory goes with it).
+// engine generation (nvl_crc32c_shutdown) or the needed size changes.
 struct HostPipe {
   int device = -1;
   uint64_t gen = 0;
@@ -372,7 +383,70 @@ struct HostPipe {
     return true;
   }
 };
-thread_local HostPipe t_pipe;
+
+// Everything a thread acquires for the host-resident entry points: one
+// non-blocking stream per device (a stream per call would also mean a
+// counter block per call), the pinned staging buffer and the fixed_host
+// pipe.  Registered globally so nvl_crc32c_shutdown can free what every
+// thread holds; a thread's own resources are freed when it exits (the
+// calling thread's thread_local destructors run before exit()'s atexit
+// handlers and static destructors, so the HIP runtime is still up).
+struct ThreadRes;
+std::mutex g_tr_mu;
+std::vector<ThreadRes*> g_tr;
+
+struct ThreadRes {
+  hipStream_t st[kMaxDevices] = {};
+  Staging staging;
+  HostPipe pipe;
+  bool registered = false;
+
+  void enroll() {
+    if (registered) return;
+    std::lock_guard<std::mutex> lk(g_tr_mu);
+    g_tr.push_back(this);
+    registered = true;
+  }
+  // Caller holds g_tr_mu or is the owning thread with no shutdown running.
+  void release() {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (int d = 0; d < kMaxDevices; ++d) {
+      if (!st[d]) continue;
+      (void)hipSetDevice(d);
+      (void)hipStreamSynchronize(st[d]);
+      forget_counter(d, st[d]);
+      (void)hipStreamDestroy(st[d]);
+      st[d] = nullptr;
+    }
+    if (pipe.device >= 0) (void)hipSetDevice(pipe.device);
+    pipe.release();
+    staging.release();
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  ~ThreadRes() {
+    std::lock_guard<std::mutex> lk(g_tr_mu);
+    if (registered) {
+      g_tr.erase(std::find(g_tr.begin(), g_tr.end(), this));
+      release();
+    }
+  }
+  hipStream_t stream(int device) {
+    if (device < 0 || device >= kMaxDevices) return nullptr;
+    enroll();
+    if (!st[device]) {
+      int prev = -1;
+      (void)hipGetDevice(&prev);
+      if (prev != device) (void)hipSetDevice(device);
+      if (hipStreamCreateWithFlags(&st[device], hipStreamNonBlocking) != hipSuccess) st[device] = nullptr;
+      if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    }
+    return st[device];
+  }
+};
+thread_local ThreadRes t_res;
+
+hipStream_t thread_stream(int device) { return t_res.stream(device); }
 
 }  // namespace
 }  // namespace nvl
@@ -404,6 +478,14 @@ int nvl_crc32c_init(int device) {
 int nvl_crc32c_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_generation.fetch_add(1, std::memory_order_acq_rel);
+  {  // every thread's streams, staging and slabs (threads re-create them on their next call)
+    std::lock_guard<std::mutex> tk(g_tr_mu);
+    for (ThreadRes* r : g_tr) {
+      r->release();
+      r->registered = false;
+    }
+    g_tr.clear();
+  }
   for (int d = 0; d < kMaxDevices; ++d) {
     DeviceState* s = g_state[d].exchange(nullptr);
     if (s) {
@@ -453,18 +535,35 @@ size_t nvl_crc32c_batch_workspace_bytes(uint64_t n) {
 int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
                          uint32_t init_all, uint32_t* out, uint32_t flags, void* workspace, size_t workspace_bytes,
                          void* stream) {
-  int rc = NVL_CRC32C_OK;
-  DeviceState* s = current_state(&rc);
+  int dev = -1;
+  int rc = stream_device(static_cast<hipStream_t>(stream), &dev);
+  if (rc != NVL_CRC32C_OK) return rc;
+  DeviceState* s = state_for(dev, &rc);
   if (!s) return rc;
   return do_fixed(s, base, stride, len, n, init, init_all, out, flags, workspace, workspace_bytes,
                   static_cast<hipStream_t>(stream));
 }
 
+int nvl_crc32c_fixed_dev_timed(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
+                               uint32_t init_all, uint32_t* out, uint32_t flags, void* workspace,
+                               size_t workspace_bytes, void* stream, void* start_event, void* stop_event) {
+  int dev = -1;
+  int rc = stream_device(static_cast<hipStream_t>(stream), &dev);
+  if (rc != NVL_CRC32C_OK) return rc;
+  DeviceState* s = state_for(dev, &rc);
+  if (!s) return rc;
+  return do_fixed(s, base, stride, len, n, init, init_all, out, flags, workspace, workspace_bytes,
+                  static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
+                  static_cast<hipEvent_t>(stop_event));
+}
+
 int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64_t* lengths, const uint32_t* init,
                          uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags, void* workspace,
                          size_t workspace_bytes, void* stream) {
-  int rc = NVL_CRC32C_OK;
-  DeviceState* s = current_state(&rc);
+  int dev = -1;
+  int rc = stream_device(static_cast<hipStream_t>(stream), &dev);
+  if (rc != NVL_CRC32C_OK) return rc;
+  DeviceState* s = state_for(dev, &rc);
   if (!s) return rc;
   return do_batch(s, base, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
                   static_cast<hipStream_t>(stream));
@@ -485,7 +584,7 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   }
   const size_t meta_off = align_up(data_bytes, 256);
   const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
-  uint8_t* hst = static_cast<uint8_t*>(t_staging.get(total));
+  uint8_t* hst = static_cast<uint8_t*>(t_res.staging.get(total));
   if (!hst) return NVL_CRC32C_EHIP;
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hst + meta_off);
   uint64_t* hlen = hoff + n;
@@ -570,7 +669,7 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   const uint64_t wbytes = hi - lo;
   const size_t meta_off = align_up(wbytes, 256);
   const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
-  uint8_t* hst = static_cast<uint8_t*>(t_staging.get(total));
+  uint8_t* hst = static_cast<uint8_t*>(t_res.staging.get(total));
   if (!hst) return NVL_CRC32C_EHIP;
   hipStream_t st = thread_stream(s->device);
   if (!st) return NVL_CRC32C_EHIP;
@@ -619,12 +718,12 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
   per = std::min<uint64_t>(per, n);
   const uint64_t slab_bytes = (per - 1) * stride + len;
   const size_t ws = fixed_ws_bytes(len, per, s->num_cu);
-  if (!t_pipe.get(s->device, align_up(slab_bytes, 256) + per * 8 + ws + 512)) {
-    t_pipe.release();
+  if (!t_res.pipe.get(s->device, align_up(slab_bytes, 256) + per * 8 + ws + 512)) {
+    t_res.pipe.release();
     return NVL_CRC32C_EHIP;
   }
-  hipStream_t* st = t_pipe.st;
-  uint8_t* dbuf[2] = {t_pipe.buf[0], t_pipe.buf[1]};
+  hipStream_t* st = t_res.pipe.st;
+  uint8_t* dbuf[2] = {t_res.pipe.buf[0], t_res.pipe.buf[1]};
   uint32_t* dout[2] = {nullptr, nullptr};
   uint32_t* dini[2] = {nullptr, nullptr};
   void* dws[2] = {nullptr, nullptr};

@@ -110,6 +110,11 @@ uint32_t block_handles(const uint8_t* data, uint64_t size, std::vector<nvl_block
                !(p = get_varint(p, limit, 28, &value_len))) {
       return NVL_TABLE_BAD_INDEX_ENTRY;
     }
+    // GetVarint32PtrFallback (util/coding.cc:112-129) accumulates into a
+    // uint32_t: a 5-byte varint's high bits are dropped, not rejected.
+    shared = (uint32_t)shared;
+    non_shared = (uint32_t)non_shared;
+    value_len = (uint32_t)value_len;
     // block.cc:70 (a 64-bit sum: the reference's uint32_t sum could wrap and read past the block)
     if ((uint64_t)(limit - p) < non_shared + value_len || key_len < shared)
       return NVL_TABLE_BAD_INDEX_ENTRY;
@@ -342,6 +347,27 @@ int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_bloc
   const uint8_t* meta_data = contents(meta_h);
   if (meta_data && meta_data[meta_h.size] == 0) block_handles(meta_data, meta_h.size, &meta_blocks, &meta_bad);
 
+  if (!blocks) {
+    // Size query: the list's length depends only on the index and metaindex
+    // verdicts, so only those two blocks are checked (host CRC) -- no batch.
+    const nvl_block_handle two[2] = {index_h, meta_h};
+    uint8_t v2[2];
+    const int rq = nvl_sstable_verify_blocks(f, file_len, two, 2, v2, nullptr, flags | NVL_FRAMING_HOST);
+    if (rq != NVL_CRC32C_OK) return rq;
+    size_t cnt = 1;
+    if (v2[0] != NVL_BLOCK_OK) {
+      *table_status = NVL_TABLE_INDEX_UNREADABLE;
+    } else if (index_data[index_h.size] != 0) {
+      *table_status = NVL_TABLE_COMPRESSED_INDEX;
+    } else {
+      const bool meta_ok = v2[1] == NVL_BLOCK_OK && meta_data[meta_h.size] == 0;
+      cnt += 1 + (meta_ok ? meta_blocks.size() : 0) + data_h.size();
+      *table_status = index_parse;
+    }
+    *n_blocks = cnt;
+    return NVL_CRC32C_OK;
+  }
+
   // One CRC batch: index, metaindex, then every decodable in-file handle.
   std::vector<nvl_block_handle> all;
   all.reserve(2 + meta_blocks.size() + data_h.size());
@@ -378,7 +404,6 @@ int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_bloc
     for (const nvl_table_block& t : out) b += t.verdict != NVL_BLOCK_OK;
     *n_bad = b;
   }
-  if (!blocks) return NVL_CRC32C_OK;
   if (out.size() > cap) return NVL_CRC32C_ENOSPC;
   if (!out.empty()) memcpy(blocks, out.data(), out.size() * sizeof(nvl_table_block));
   return NVL_CRC32C_OK;

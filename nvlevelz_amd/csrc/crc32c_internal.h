@@ -36,6 +36,11 @@ struct LaunchCtx {
   int num_cu;
   const uint32_t* tables;  // device blob
   uint32_t* counter;       // the stream's counter block (fused kernels), or nullptr
+  // Measurement only (nvl_crc32c_fixed_dev_timed): recorded by the call's
+  // first / last kernel dispatch itself (hipExtLaunchKernel), so they time the
+  // kernels alone and add no marker packet between back-to-back launches.
+  hipEvent_t ev_start = nullptr;
+  hipEvent_t ev_stop = nullptr;
 };
 
 void build_device_tables(uint32_t* words /* kTableWords */);

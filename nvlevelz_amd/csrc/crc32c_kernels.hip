@@ -31,6 +31,7 @@
 // data-dependent indices never bank-conflicts (bank = lane%32).  Address of
 // table t, byte b, lane l:  (t>>1)<<16 | b<<8 | (t&1)<<7 | (l&31)<<2, formed
 // with ONE v_perm_b32 per lookup from the data word and a per-lane base.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -1464,10 +1465,14 @@ hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64
 }
 
 static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, const uint32_t* tables,
-                                      uint32_t* out, uint32_t flags, hipStream_t st) {
+                                      uint32_t* out, uint32_t flags, hipStream_t st, hipEvent_t ev_stop = nullptr) {
   const uint32_t tpb = 256;
-  hipLaunchKernelGGL(dev::crc32c_fixup_kernel, dim3((nw + tpb - 1) / tpb), dim3(tpb), 0, st, recs, nw,
-                     tables, out, flags);
+  if (ev_stop)
+    hipExtLaunchKernelGGL(dev::crc32c_fixup_kernel, dim3((nw + tpb - 1) / tpb), dim3(tpb), 0, st, nullptr, ev_stop,
+                          0u, recs, nw, tables, out, flags);
+  else
+    hipLaunchKernelGGL(dev::crc32c_fixup_kernel, dim3((nw + tpb - 1) / tpb), dim3(tpb), 0, st, recs, nw,
+                       tables, out, flags);
   return hipGetLastError();
 }
 
@@ -1489,16 +1494,26 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   const bool aligned = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
   dev::KArgs ka{out, flags, J > 1 ? recs : nullptr, lc.tables, nullptr};
-  if (aligned)
-    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
-                       ka);
-  else
-    hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0,
-                       lc.stream, g,
-                       ka);
+  hipEvent_t stop_main = J == 1 ? lc.ev_stop : nullptr;  // else the fix-up records it
+  const bool timed = lc.ev_start || stop_main;
+  if (aligned) {
+    if (timed)
+      hipExtLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream,
+                            lc.ev_start, stop_main, 0u, g, ka);
+    else
+      hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
+                         ka);
+  } else {
+    if (timed)
+      hipExtLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kWave * dev::kGenWaves),
+                            0, lc.stream, lc.ev_start, stop_main, 0u, g, ka);
+    else
+      hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0,
+                         lc.stream, g, ka);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || J == 1) return e;
-  return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream, lc.ev_stop);
 }
 
 size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {

@@ -169,11 +169,17 @@ def log_scan(image: BytesLike, *, start: int = 0, checksum: bool = True,
     [(kind, header_offset, payload_length, type)] ending with ("eof", ...)."""
     ptr, n, _keep = _ro(image)
     cnt = ctypes.c_size_t(0)
-    _check(_lib.lib.nvl_log_scan(ptr, n, start, int(checksum), None, 0, ctypes.byref(cnt), _flags(host)),
-           "log_scan")
-    ev = (_lib.LogEvent * max(cnt.value, 1))()
-    _check(_lib.lib.nvl_log_scan(ptr, n, start, int(checksum), ev, cnt.value, ctypes.byref(cnt), _flags(host)),
-           "log_scan")
+    # One scan when the guess fits (records of >= ~256 B on average); a log of
+    # tinier records is scanned again with the exact count the first call reported.
+    cap = n // 256 + 64
+    while True:
+        ev = (_lib.LogEvent * cap)()
+        rc = _lib.lib.nvl_log_scan(ptr, n, start, int(checksum), ev, cap, ctypes.byref(cnt), _flags(host))
+        if rc == _lib.ENOSPC and cnt.value > cap:
+            cap = cnt.value
+            continue
+        _check(rc, "log_scan")
+        break
     return [(LOG_KIND[e.kind], e.offset, e.length, e.type) for e in ev[:cnt.value]]
 
 

@@ -78,6 +78,11 @@ class _Port:
                                                ctypes.c_uint64, ctypes.c_uint64,
                                                ctypes.c_void_p, ctypes.c_int,
                                                ctypes.c_int]
+        lib.oracle_crc32c_fixed_mt_reps.restype = ctypes.c_int
+        lib.oracle_crc32c_fixed_mt_reps.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                                    ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_void_p, ctypes.c_int,
+                                                    ctypes.c_int, ctypes.c_uint64]
         self.lib = lib
 
     # -- util/crc32c.h API -------------------------------------------------
@@ -151,10 +156,11 @@ class _Port:
         return self.lib.oracle_digest(crcs.ctypes.data, crcs.size)
 
     def fixed_mt(self, buf: np.ndarray, stride: int, length: int, n: int,
-                 threads: int, table: bool = False) -> np.ndarray:
+                 threads: int, table: bool = False, reps: int = 1) -> np.ndarray:
+        """reps passes over each thread's contiguous share (timed baselines)."""
         out = np.empty(n, dtype=np.uint32)
-        rc = self.lib.oracle_crc32c_fixed_mt(buf.ctypes.data, stride, length, n,
-                                             out.ctypes.data, threads, int(table))
+        rc = self.lib.oracle_crc32c_fixed_mt_reps(buf.ctypes.data, stride, length, n,
+                                                  out.ctypes.data, threads, int(table), reps)
         if rc != 0:
             raise RuntimeError("oracle_crc32c_fixed_mt failed")
         return out
@@ -182,6 +188,10 @@ class _Ref:
         lib.ref_crc32c_fixed_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
                                             ctypes.c_uint64, ctypes.c_uint64,
                                             ctypes.c_void_p, ctypes.c_int]
+        lib.ref_crc32c_fixed_mt_reps.restype = ctypes.c_int
+        lib.ref_crc32c_fixed_mt_reps.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_uint64, ctypes.c_uint64,
+                                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
         self.lib = lib
         self.path = path
 
@@ -203,10 +213,11 @@ class _Ref:
         return self.lib.ref_crc32c_unmask(m & 0xFFFFFFFF)
 
     def fixed_mt(self, buf: np.ndarray, stride: int, length: int, n: int,
-                 threads: int) -> np.ndarray:
+                 threads: int, reps: int = 1) -> np.ndarray:
+        """reps passes over each thread's contiguous share (timed baselines)."""
         out = np.empty(n, dtype=np.uint32)
-        rc = self.lib.ref_crc32c_fixed_mt(buf.ctypes.data, stride, length, n,
-                                          out.ctypes.data, threads)
+        rc = self.lib.ref_crc32c_fixed_mt_reps(buf.ctypes.data, stride, length, n,
+                                               out.ctypes.data, threads, reps)
         if rc != 0:
             raise RuntimeError("ref_crc32c_fixed_mt failed")
         return out

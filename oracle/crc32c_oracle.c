@@ -241,19 +241,22 @@ uint32_t oracle_digest(const uint32_t* crcs, uint64_t n) {
  * (interleaving caused false sharing).  which: 0 = dispatching
  * Extend (SSE when available), 1 = table path. */
 typedef struct {
-  const uint8_t* base; uint64_t stride, len, lo, hi; uint32_t* out; int which;
+  const uint8_t* base; uint64_t stride, len, lo, hi; uint32_t* out; int which; uint64_t reps;
 } oracle_job_t;
 
 static void* oracle_job(void* arg) {
   oracle_job_t* j = (oracle_job_t*)arg;
-  for (uint64_t i = j->lo; i < j->hi; ++i)
-    j->out[i] = j->which ? oracle_crc32c_extend_table(0, j->base + i * j->stride, (size_t)j->len)
-                         : oracle_crc32c_extend(0, j->base + i * j->stride, (size_t)j->len);
+  for (uint64_t r = 0; r < j->reps; ++r)
+    for (uint64_t i = j->lo; i < j->hi; ++i)
+      j->out[i] = j->which ? oracle_crc32c_extend_table(0, j->base + i * j->stride, (size_t)j->len)
+                           : oracle_crc32c_extend(0, j->base + i * j->stride, (size_t)j->len);
   return 0;
 }
 
-int oracle_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
-                           uint64_t n, uint32_t* out, int threads, int which) {
+/* reps passes over each thread's share (a timed baseline pays the thread
+ * start-up once). */
+int oracle_crc32c_fixed_mt_reps(const uint8_t* base, uint64_t stride, uint64_t len,
+                                uint64_t n, uint32_t* out, int threads, int which, uint64_t reps) {
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   pthread_t tid[256];
@@ -264,11 +267,16 @@ int oracle_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
     jobs[t].base = base; jobs[t].stride = stride; jobs[t].len = len;
     jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
     jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
-    jobs[t].out = out; jobs[t].which = which;
+    jobs[t].out = out; jobs[t].which = which; jobs[t].reps = reps;
   }
   for (int t = 1; t < threads; ++t)
     if (pthread_create(&tid[t], 0, oracle_job, &jobs[t]) != 0) return -1;
   oracle_job(&jobs[0]);
   for (int t = 1; t < threads; ++t) pthread_join(tid[t], 0);
   return 0;
+}
+
+int oracle_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
+                           uint64_t n, uint32_t* out, int threads, int which) {
+  return oracle_crc32c_fixed_mt_reps(base, stride, len, n, out, threads, which, 1);
 }

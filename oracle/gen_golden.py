@@ -206,6 +206,42 @@ def configs(do_cfg4: bool) -> dict:
     return out
 
 
+def cfg5() -> dict:
+    """Config 5 (BASELINE.json configs[4]): 10^7 x 4096 B of the splitmix64
+    stream seeded 0x5EED0005, buffer i = stream bytes [4096 i, 4096 i + 4096)
+    (buffer i lives on GPU i mod G, generated in place there).
+    41 GB never fits here at once: the stream is generated in 10^5-block
+    chunks and checksummed by the oracle's C restatement (oracle/crc32c_oracle.c,
+    the port of port/port_posix_sse.cc:69-126).  The restatement is pinned
+    first: the 10^5-block prefix (and every 10th chunk) is also checksummed by
+    the REFERENCE's own build (oracle/_ref, util/crc32c.cc +
+    port/port_posix_sse.cc) and must agree CRC for CRC.  The digest is
+    Value() over the little-endian array of all 10^7 CRCs in global order,
+    the same definition as configs 2-4.  Per-10^6-block sub-digests are kept
+    too, so a shard test can check a part without the whole."""
+    p = oracle.port()
+    r = oracle.ref("sse")
+    n, L, chunk = 10_000_000, 4096, 100_000
+    th = min(8, os.cpu_count() or 1)
+    crc = np.empty(n, dtype=np.uint32)
+    part = aligned_buffer(chunk * L)
+    ref_checked = 0
+    for k, s in enumerate(range(0, n, chunk)):
+        part[:] = p.fill(0x5EED0005, s * L, part.size)
+        crc[s:s + chunk] = p.fixed_mt(part, L, L, chunk, th)
+        if k % 10 == 0:
+            want = r.fixed_mt(part, L, L, chunk, th)
+            assert np.array_equal(crc[s:s + chunk], want), f"restatement != reference on chunk {k}"
+            ref_checked += chunk
+    sub = [p.digest(crc[s:s + 1_000_000]) for s in range(0, n, 1_000_000)]
+    return {"seed": 0x5EED0005, "n": n, "len": L, "stride": L,
+            "crc_first": [int(x) for x in crc[:8]], "crc_last": int(crc[-1]),
+            "digest": p.digest(crc), "sub_digest_blocks": 1_000_000, "sub_digests": [int(x) for x in sub],
+            "ref_checked_blocks": ref_checked,
+            "how": "oracle restatement (port) over all blocks; reference build (oracle/_ref) on every 10th "
+                   "10^5-block chunk incl. the prefix, identical"}
+
+
 def table_cases() -> dict:
     """SSTable scenarios (tests/table_cases.py) scanned by the REFERENCE's own
     Footer::DecodeFrom, ReadBlock and Block::Iter (table/format.cc,
@@ -242,9 +278,24 @@ def main() -> None:
         with open(os.path.join(GOLDEN, f"{name}.json"), "w") as f:
             json.dump(d, f, separators=(",", ":"))
         print("wrote", name)
+    if "cfg5" in only:  # added to the existing configs.json (10^7 blocks: minutes of CPU)
+        path = os.path.join(GOLDEN, "configs.json")
+        with open(path) as f:
+            d = json.load(f)
+        d["cfg5"] = cfg5()
+        with open(path, "w") as f:
+            json.dump(d, f, indent=1)
+        print("cfg5 digest", hex(d["cfg5"]["digest"]), "crc_last", hex(d["cfg5"]["crc_last"]))
     if only and "configs" not in only:
         return
     d = configs(not args.no_cfg4)
+    try:  # keep a cfg5 made earlier (--only cfg5)
+        with open(os.path.join(GOLDEN, "configs.json")) as f:
+            old = json.load(f)
+        if "cfg5" in old:
+            d["cfg5"] = old["cfg5"]
+    except (OSError, ValueError):
+        pass
     d["provenance"] = provenance
     with open(os.path.join(GOLDEN, "configs.json"), "w") as f:
         json.dump(d, f, indent=1)

@@ -48,21 +48,24 @@ uint32_t ref_accelerated_crc32c(uint32_t init, const void* data, size_t n) {
 }
 
 // Batch driver for baselines: buffer i = base + i*stride, len bytes, Value().
+// `reps` passes over each thread's contiguous share, so a timed baseline
+// pays the thread start-up once, not per pass.
 struct RefJob {
-  const uint8_t* base; uint64_t stride, len, lo, hi; uint32_t* out;
+  const uint8_t* base; uint64_t stride, len, lo, hi; uint32_t* out; uint64_t reps;
 };
 
 static void* ref_job(void* a) {
   RefJob* j = static_cast<RefJob*>(a);
-  for (uint64_t i = j->lo; i < j->hi; ++i)
-    j->out[i] = leveldb::crc32c::Value(
-        reinterpret_cast<const char*>(j->base + i * j->stride), j->len);
+  for (uint64_t r = 0; r < j->reps; ++r)
+    for (uint64_t i = j->lo; i < j->hi; ++i)
+      j->out[i] = leveldb::crc32c::Value(
+          reinterpret_cast<const char*>(j->base + i * j->stride), j->len);
   return nullptr;
 }
 
 __attribute__((visibility("default")))
-int ref_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
-                        uint64_t n, uint32_t* out, int threads) {
+int ref_crc32c_fixed_mt_reps(const uint8_t* base, uint64_t stride, uint64_t len,
+                             uint64_t n, uint32_t* out, int threads, uint64_t reps) {
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   pthread_t tid[256];
@@ -70,13 +73,19 @@ int ref_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
   (void)leveldb::crc32c::Value("", 0);  // resolve the static probe once
   for (int t = 0; t < threads; ++t) {
     jobs[t] = RefJob{base, stride, len, n * (uint64_t)t / (uint64_t)threads,
-                     n * (uint64_t)(t + 1) / (uint64_t)threads, out};
+                     n * (uint64_t)(t + 1) / (uint64_t)threads, out, reps};
   }
   for (int t = 1; t < threads; ++t)
     if (pthread_create(&tid[t], nullptr, ref_job, &jobs[t]) != 0) return -1;
   ref_job(&jobs[0]);
   for (int t = 1; t < threads; ++t) pthread_join(tid[t], nullptr);
   return 0;
+}
+
+__attribute__((visibility("default")))
+int ref_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
+                        uint64_t n, uint32_t* out, int threads) {
+  return ref_crc32c_fixed_mt_reps(base, stride, len, n, out, threads, 1);
 }
 
 }  // extern "C"

@@ -36,7 +36,16 @@ def handle(off: int, size: int) -> bytes:
     return varint(off) + varint(size)
 
 
-def block(entries: list[tuple[bytes, bytes]], restart_interval: int, force_varint: bool = False) -> bytes:
+def varint32_wrapped(x: int) -> bytes:
+    """x < 2^28 as a 5-byte varint whose last byte carries bit 32: the
+    reference's GetVarint32PtrFallback (util/coding.cc:112-129) accumulates
+    into a uint32_t and drops it, so it still decodes x."""
+    return bytes([(x & 127) | 128, ((x >> 7) & 127) | 128, ((x >> 14) & 127) | 128, ((x >> 21) & 127) | 128,
+                  ((x >> 28) & 15) | 0x10])
+
+
+def block(entries: list[tuple[bytes, bytes]], restart_interval: int, force_varint: bool = False,
+          wrap32: bool = False) -> bytes:
     """BlockBuilder layout (table/block_builder.cc): shared | non_shared |
     value_len (varint32) | key delta | value, then the restart array."""
     out = bytearray()
@@ -51,6 +60,8 @@ def block(entries: list[tuple[bytes, bytes]], restart_interval: int, force_varin
             shared += 1
         if force_varint:  # multi-byte encodings of small values (still valid varints)
             out += bytes([shared | 128, 0]) + bytes([(len(k) - shared) | 128, 0]) + bytes([len(v) | 128, 0])
+        elif wrap32:  # 5-byte encodings with bit 32 set (truncated by the reference's decoder)
+            out += varint32_wrapped(shared) + varint32_wrapped(len(k) - shared) + varint32_wrapped(len(v))
         else:
             out += varint(shared) + varint(len(k) - shared) + varint(len(v))
         out += k[shared:] + v
@@ -105,7 +116,7 @@ def build(port, spec: dict) -> tuple[bytes, dict]:
         ents[i] = (ents[i][0], handle(data[i][0][0], 1 << 40))
     if mode == "overlap" and len(ents) > 1:  # a handle straddling two blocks (reads, checksum mismatch)
         ents[0] = (ents[0][0], handle(data[0][0][0] + 1, data[0][0][1]))
-    idx = block(ents, 1, force_varint=(mode == "varint"))
+    idx = block(ents, 1, force_varint=(mode == "varint"), wrap32=(mode == "varint32_wrap"))
     if mode == "bad_entry" and ents:       # shared > previous key length -> "bad entry in block"
         cut = int(rng.integers(0, len(ents)))
         body, starts = b"", []
@@ -211,6 +222,7 @@ def named() -> list[dict]:
     add("empty_index", index_mode="empty")
     add("compressed_index", index_mode="compressed")
     add("restart0_past", index_mode="restart0_past", nblocks=1)
+    add("varint32_wrap", index_mode="varint32_wrap", nblocks=5)
     return c
 
 

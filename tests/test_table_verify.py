@@ -53,11 +53,15 @@ def verify(L, img: bytes, flags: int):
     st = ctypes.c_uint32(0)
     nb = ctypes.c_uint64(0)
     lib = L.lib
+    # the size query (blocks = NULL) checks only the index and metaindex on the
+    # host, and must still give the exact count and table status
     assert lib.nvl_sstable_verify_table(img, len(img), None, 0, ctypes.byref(n), ctypes.byref(st),
                                         ctypes.byref(nb), flags) == 0
+    q_n, q_st = n.value, st.value
     arr = (L.TableBlock * max(n.value, 1))()
     assert lib.nvl_sstable_verify_table(img, len(img), arr, n.value, ctypes.byref(n), ctypes.byref(st),
                                         ctypes.byref(nb), flags) == 0
+    assert (q_n, q_st) == (n.value, st.value)
     blocks = [(a.offset, a.size, a.role, a.verdict) for a in arr[:n.value]]
     assert nb.value == sum(b[3] != 0 for b in blocks)
     return st.value, blocks

@@ -15,7 +15,7 @@ rc=$?; echo "[gpu_check] pytest rc=$rc"; tail -3 $OUT/pytest_gpu_$TAG.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1
 rc=$?; echo "[gpu_check] smoke rc=$rc"; tail -1 $OUT/smoke_$TAG.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python bench.py --e2e > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+timeout -k 10 400 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
 rc=$?; echo "[gpu_check] bench rc=$rc"; cat $OUT/bench_$TAG.json
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python tools/bench_configs.py > $OUT/configs_$TAG.jsonl 2> $OUT/configs_$TAG.err

@@ -45,8 +45,9 @@ struct LaunchCtx {
 
 void build_device_tables(uint32_t* words /* kTableWords */);
 
+// ws: fixed_recs_bytes() of workspace (unit records, then head contributions).
 hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
-                        const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs);
+                        const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* ws);
 size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n);  // workspace of launch_fixed
 size_t var_recs_bytes(int num_cu);                               // record part of launch_var's workspace
 size_t var_unit_map_bytes(int num_cu);                           // unit map part of launch_var's workspace
@@ -58,15 +59,17 @@ hipError_t launch_var_plan_small(const LaunchCtx& lc, const uint64_t* lengths, u
                                  uint64_t* unit_first);
 hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st);
 // have_unit_map: unit_first already written (small plan); otherwise built here.
+// hc: n u32 of workspace (head contributions, written by the head kernel
+// that every variable-length call launches first).
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
-                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, bool have_unit_map);
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, bool have_unit_map);
 
 // Plan + checksum + fix-up in one launch (n <= kPlanSmallMax, lc.counter
 // set); recs: the launch_var workspace records (hold the edge records).
 hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                             uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
-                            Rec* recs);
+                            Rec* recs, uint32_t* hc);
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

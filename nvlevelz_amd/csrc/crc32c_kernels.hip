@@ -46,6 +46,17 @@ constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWave * kWavesPerWG;  // 1024
 constexpr uint32_t kChunk = 4096;
 constexpr uint32_t kUnitsPerWG = 64;  // work units per workgroup (scheduler B)
+// Overhang: a buffer's first chunk may hold up to kOver bytes more than 4096
+// (a 4097..4112-byte buffer is ONE pass -- the n+1-byte CRC of an SSTable
+// data block of 4096..4111 bytes, table/format.cc:90-92); the extra bytes are
+// checksummed as one 16-byte piece beside the chunk's 64 pieces.
+constexpr uint32_t kOver = 16;
+
+// Chunks of a buffer of L bytes: END-aligned 4096-byte chunks, the first one
+// 1..4096+kOver bytes long (tests/kernel_model.py chunks_of).
+__host__ __device__ __forceinline__ uint32_t chunks_for(uint64_t L) {
+  return L <= kChunk + kOver ? 1u : (uint32_t)((L - kOver + kChunk - 1) / kChunk);
+}
 
 // LDS image (bytes)
 // The operator tables sit first so that every table offset of a lookup fits
@@ -64,6 +75,16 @@ static_assert(kLdsBytes <= 160u * 1024u, "LDS image exceeds 160 KiB");
 constexpr uint32_t kGSlice = 0, kGComb = 1024, kGX2n = 1024 + 6144 + 1024;  // comb, sh4096 contiguous
 
 // ---------------------------------------------------------------------------
+// Wave-uniform copies (lane 0's value in SGPRs).  readfirstlane returns int:
+// each half goes through uint32_t so that a low half >= 2^31 is not
+// sign-extended into the high half (a device address usually has bit 31 set).
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | (uint64_t)uniform_u32((uint32_t)v);
+}
+
 // cross-lane helpers (all called with EXEC = all 64 lanes)
 __device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
@@ -274,6 +295,11 @@ struct KArgs {
   Rec* recs;  // 2 per work unit: [2u] = head portion, [2u+1] = tail portion (or nullptr)
   const uint32_t* tables;
   uint32_t* counter;  // the stream's done counter (fused variable kernel); zero between launches
+  // Head contributions (kGeneral): hc[i] = buffer i's partial first chunk,
+  // normalized to the buffer end, written by crc32c_head_kernel before the
+  // body kernel runs (0 for a buffer without one); nullptr when no buffer of
+  // the batch has a partial first chunk.
+  uint32_t* hc;
 };
 
 // Global work units: the grid's NU = gridDim.x * kUnitsPerWG units split the
@@ -305,6 +331,12 @@ struct FixedGeom {
   }
   __device__ __forceinline__ void locate_unit(uint32_t, uint64_t t, uint64_t& i, uint32_t& c) const {
     locate(t, i, c);
+  }
+  // Buffer i's start, length and ~init in this lane (head kernel).
+  __device__ __forceinline__ void lane_meta(uint64_t i, uintptr_t& p, uint64_t& L, uint32_t& sx) const {
+    p = (uintptr_t)(base + i * stride);
+    L = len;
+    sx = ~(init ? init[i] : init_all);
   }
   __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo(T, u); }
   __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
@@ -338,9 +370,13 @@ struct VarGeom {
   }
   __device__ __forceinline__ BufInfo info(uint64_t i) const {
     const uint64_t L = ldc(lengths, i);
-    const uint32_t J = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
     const uint32_t ini = init ? ldc(init, i) : init_all;
-    return BufInfo{base + ldc(offsets, i), L, J, ~ini};
+    return BufInfo{base + ldc(offsets, i), L, chunks_for(L), ~ini};
+  }
+  __device__ __forceinline__ void lane_meta(uint64_t i, uintptr_t& p, uint64_t& L, uint32_t& sx) const {
+    p = (uintptr_t)(base + offsets[i]);
+    L = lengths[i];
+    sx = ~(init ? init[i] : init_all);
   }
   __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo(T, u); }
   __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
@@ -349,20 +385,35 @@ struct VarGeom {
 };
 
 // Load modes: kAligned = 16-B aligned buffer whose length is a multiple of 4096
-// (every chunk full, no masking: configs 2, 4, 5); kGeneral = any alignment and
-// length (partial head chunk, realignment, predicated loads: config 3).
-enum LoadMode : int { kAligned = 0, kGeneral = 1 };
+// (every chunk full, no masking: configs 2, 4, 5); kGeneral = the full
+// 4096-byte chunks of buffers of any alignment and length (realignment, the
+// overhang); kHead = partial first chunks (they start before the buffer:
+// predicated loads, masking), run by their own kernel so that the body
+// kernel's registers never hold the masking code's (86 vs 128+ VGPRs).
+enum LoadMode : int { kAligned = 0, kGeneral = 1, kHead = 2 };
+
+// A buffer's first chunk is a head chunk when it starts before the buffer
+// (partial: 1..4095 bytes) or the buffer is shorter than 4 bytes (bytewise).
+__host__ __device__ __forceinline__ bool head_first(uint64_t L) {
+  return L < 4 || L - (uint64_t)kChunk * (chunks_for(L) - 1u) < kChunk;
+}
 
 // Registers of one chunk as loaded.  Load j (j = 0..3) is one coalesced 1 KiB
 // wave load of chunk bytes [1024j, 1024j+1024) in a permuted lane order: lane
 // (a, b) = (lane >> 4, lane & 15) takes the 16 B at 1024j + 64b + 16a, so that
 // the 4x4 exchange across 16-lane rows in row_transpose leaves lane P holding
 // the 64 contiguous bytes [64P, 64P+64) -- piece P = lane.  In kGeneral the
-// loads start at the aligned address below the chunk start (16-B for a head
-// chunk, 4-B for a body chunk) and d[16..19] holds the bytes just past the
-// last piece (wave-uniform, scalar loaded).
+// loads start at the 4-byte aligned address A4 below the chunk start (gfx950
+// serves 4-B aligned dwordx4 at the 16-B aligned rate, byte-misaligned ones at
+// ~2/3: tools/diag/ldpat.hip, profiles/r02_ldpat.jsonl).  e[] is one more
+// 16-byte load by two lanes: lane 63 reads the 16 bytes ending at A4 + 4100
+// (e[3] = the dword just past the last piece), lane 0 the 16 bytes before A4
+// on a chunk with an overhang.  Vector loads, not scalar ones: an s_load in
+// flight would make every LDS wait of the chains wait for it too (both count
+// in lgkmcnt, and scalar loads return out of order).
 struct Chunk {
-  uint32_t d[20];
+  uint32_t d[16];
+  uint32_t e[4];
 };
 
 __device__ __forceinline__ uintptr_t chunk_end(const BufInfo& bi, uint32_t c) {
@@ -372,6 +423,11 @@ __device__ __forceinline__ uintptr_t chunk_end(const BufInfo& bi, uint32_t c) {
 // Byte offset of the lane's 16 B within each 1 KiB load.
 __device__ __forceinline__ uint32_t lane_load_off(int lane) {
   return ((uint32_t)(lane & 15) << 6) | ((uint32_t)(lane >> 4) << 4);
+}
+
+// A wave-uniform dword through the constant address space (s_load).
+__device__ __forceinline__ uint32_t sload_u32(uintptr_t a) {
+  return *reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(a);
 }
 
 template <int M>
@@ -400,40 +456,46 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
       ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
     }
   } else {
-    if (bi.len < 4) return;  // tiny path reads its own bytes
-    const uintptr_t p = (uintptr_t)bi.p;
-    if (ce - kChunk < p + 4) {
-      // Head chunk: 16-B aligned loads below the chunk start (never crossing
-      // into a page the buffer does not touch), vectors wholly before the
-      // buffer skipped; the aligned vector just past the last piece is the
-      // same for every lane: a scalar load (SGPRs) ending inside ce's granule.
-      const uint32_t m = (uint32_t)(ce & 15u);
-      const uintptr_t A = ce - kChunk - m;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uintptr_t addr = A + 1024u * (uint32_t)j + lo;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (addr + 16u > p) v = ld16(addr);
-        ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
-      }
-      u32x4 x = {0u, 0u, 0u, 0u};
-      if (m != 0) x = *reinterpret_cast<const __attribute__((address_space(4))) u32x4*>(A + kChunk);
-      ch.d[16] = x.x; ch.d[17] = x.y; ch.d[18] = x.z; ch.d[19] = x.w;
-    } else {
-      // Body chunk: every byte of [ce-4096-3, ce) lies inside the buffer, so
-      // the loads start at the DWORD-aligned address below the chunk start
-      // (gfx950 serves 4-B aligned dwordx4 at full rate, byte-misaligned at
-      // ~80 %: tools/diag/unaligned.hip); the dword past the last piece
-      // (scalar) completes lane 63.
-      const uint32_t r = (uint32_t)(ce & 3u);
-      const uintptr_t A4 = ce - kChunk - r;
+    // Four 1 KiB loads from A4, the 4-byte aligned address at or below the
+    // chunk start, plus the edge load (see Chunk).  Fault safety: only 16-B
+    // granules that hold buffer bytes are touched (asserted by
+    // tests/kernel_model.py).  kGeneral chunks start at or after the buffer
+    // start, so A4 >= floor4(p) >= p's granule g.
+    const uint32_t r = (uint32_t)(ce & 3u);
+    const uintptr_t A4 = ce - kChunk - r;
+    const uintptr_t g = (uintptr_t)bi.p & ~(uintptr_t)15;  // granule of the buffer start
+    if constexpr (M == kGeneral) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
         ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
       }
-      ch.d[16] = r ? *reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(A4 + kChunk) : 0u;
-      ch.d[17] = ch.d[18] = ch.d[19] = 0u;
+    } else {
+      // kHead: the chunk reaches below p's granule g: a slot wholly below g
+      // is not loaded (zeros); the slot straddling g is loaded from g (its
+      // words are moved into place by build_words -- not here, so that no
+      // instruction waits on this prefetch); the rest load as usual.
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uintptr_t a = A4 + 1024u * (uint32_t)j + lo;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (a + 16u > g) v = ld16(a < g ? g : a);
+        ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+      }
+    }
+    // Edge load: lane 63 when the realign needs the dword past the last
+    // piece (r != 0; the 16 bytes end in the chunk's last dword, which holds
+    // byte ce-1), lane 0 when the chunk has an overhang (kGeneral chunk 0
+    // starting after p: the 16 bytes below A4, clamped up to p's granule;
+    // build_words moves them into place).
+    // A head chunk's buffer can be shorter than those 16 bytes: lane 63's
+    // address is then clamped up to g too (edge_dword picks the dword).
+    const bool ovh = M == kGeneral && c == 0 && A4 + r > (uintptr_t)bi.p;
+    if ((lane == 63 && r != 0) || (lane == 0 && ovh)) {
+      const uintptr_t e63 = M == kHead && A4 + kChunk - 12u < g ? g : A4 + kChunk - 12u;
+      const uintptr_t ea = lane == 63 ? e63 : (A4 - 16u > g ? A4 - 16u : g);
+      const u32x4 v = ld16(ea);
+      ch.e[0] = v.x; ch.e[1] = v.y; ch.e[2] = v.z; ch.e[3] = v.w;
     }
   }
 }
@@ -460,27 +522,60 @@ __device__ __forceinline__ uint32_t next_lane(uint32_t v, uint32_t last) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)v, 0x130, 0xF, 0xF, false);
 }
 
-// Head-chunk realign for a dword shift Q (compile-time) and byte shift r:
-// out[k] = bytes [4(k+Q) + r, +4) of the lane's piece extended by nx[].
-template <int Q>
-__device__ __forceinline__ void realign_q(uint32_t (&w)[16], const uint32_t (&nx)[4], uint32_t r) {
-  uint32_t e[20];
+// Zero the bytes of a piece before the buffer start and XOR ~init (s) into the
+// 4 bytes at it: rel = bytes of the piece before the start.  Words below
+// zk = clamp(rel)/4 are zeroed, word zk keeps its bytes from the start on
+// (pm), and s lands as s << 8b in word kk = floor(rel/4) and s >> (32-8b) in
+// word kk+1 (b = rel & 3); four per-lane values, two compares per word.
+template <int NW>
+__device__ __forceinline__ void mask_inject(uint32_t (&w)[NW], int rel, uint32_t s) {
+  const int z = min(max(rel, 0), 4 * NW);
+  const int zk = z >> 2;
+  const uint32_t pm = ~0u << (8u * (uint32_t)(z & 3));
+  const int kk = rel >> 2;  // arithmetic: rel in [-3, -1] -> -1
+  const uint32_t b = (uint32_t)rel & 3u;
+  const uint32_t lo = s << (8u * b);
+  const uint32_t hi = b ? s >> (32u - 8u * b) : 0u;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) e[k] = w[k];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) e[16 + k] = nx[k];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(e[k + Q + 1], e[k + Q], r);
+  for (int k = 0; k < NW; ++k) {
+    uint32_t x = k < zk ? 0u : (k == zk ? w[k] & pm : w[k]);
+    x ^= k == kk ? lo : (k == kk + 1 ? hi : 0u);
+    w[k] = x;
+  }
 }
 
 // The lane's 16 words of piece P = lane (64 contiguous bytes), with the ~init
-// injection and, on the head chunk, the zero-masking of bytes before the
+// injection and, on a head chunk, the zero-masking of bytes before the
 // buffer start.
 template <int M>
 __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int lane, const Chunk& ch,
-                                            uint32_t (&w)[16]) {
+                                            uint32_t (&w)[16], uint32_t (&ov)[4]) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
+  if constexpr (M == kHead) {
+    // The slot straddling the start granule g was loaded from g: move its
+    // words up by q = (g - a)/4 dwords (q is the same for the whole wave: a
+    // is A4 mod 16); its words below g are before p and masked below.
+    const uintptr_t ce = chunk_end(bi, c);
+    const uintptr_t A4 = ce - kChunk - (ce & 3u);
+    const uintptr_t g = (uintptr_t)bi.p & ~(uintptr_t)15;
+    const uint32_t q = (uint32_t)((g - A4) >> 2) & 3u;
+    if (A4 < g && q != 0) {
+      const uint32_t lo = lane_load_off(lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uintptr_t a = A4 + 1024u * (uint32_t)j + lo;
+        if (a < g && a + 16u > g) {
+          uint32_t* x = w + 4 * j;
+          const uint32_t v0 = x[0], v1 = x[1], v2 = x[2];
+          x[3] = q == 1 ? v2 : (q == 2 ? v1 : v0);
+          x[2] = q == 1 ? v1 : (q == 2 ? v0 : 0u);
+          x[1] = q == 1 ? v0 : 0u;
+          x[0] = 0u;
+        }
+      }
+    }
+  }
 #if !defined(NVL_ABL_NOLOAD)
   row_transpose(w);
 #endif
@@ -488,59 +583,79 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
     if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0, word 0
   } else {
     const uintptr_t ce = chunk_end(bi, c);
-    const bool head = ce - kChunk < (uintptr_t)bi.p + 4;
-    // Shift the pieces left by sh bytes: head chunks were loaded from the 16-B
-    // aligned address below the chunk start (sh = ce & 15), body chunks from
-    // the 4-B aligned one (sh = ce & 3).  Lane P's bytes continue in lane P+1
-    // and, for lane 63, in the scalar extra.
-    const uint32_t sh = head ? (uint32_t)(ce & 15u) : (uint32_t)(ce & 3u);
-#if defined(NVL_ABL_NOREALIGN)
-    if (false) {
-#else
-    if (sh != 0) {
-#endif
-      const uint32_t r = sh & 3u;
-      if (head) {
-        uint32_t nx[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) nx[k] = next_lane(w[k], ch.d[16 + k]);
-        switch (sh >> 2) {  // wave-uniform: one straight-line variant per dword shift
-          case 0: realign_q<0>(w, nx, r); break;
-          case 1: realign_q<1>(w, nx, r); break;
-          case 2: realign_q<2>(w, nx, r); break;
-          default: realign_q<3>(w, nx, r); break;
-        }
-      } else {
-        const uint32_t nx = next_lane(w[0], ch.d[16]);
-#pragma unroll
-        for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
-        w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
-      }
-    }
+    const uintptr_t cs = ce - kChunk;
     const uintptr_t p = (uintptr_t)bi.p;
-#if defined(NVL_ABL_NOMASK)
-    if (false) {
-#else
-    if (head) {  // chunk holds the buffer head (or the tail of its ~init)
-#endif
-      // d0 = buffer start - chunk start, in (-4, 4096) for a head chunk;
-      // rel = bytes of this lane's piece (P = lane) before the buffer start.
-      // Word k keeps its bytes at or after the start and takes the ~init
-      // bytes at [rel, rel+4): both from 64-bit shifts whose clamped amounts
-      // make the out-of-range cases come out as 0 / all-ones.
-      const int d0 = (int)(int64_t)(p - (ce - kChunk));
-      const int P = (int)opaque((uint32_t)lane);
-      const int rel = min(max(d0 - 64 * P, -8), 72);
-      const uint64_t s_hi = (uint64_t)bi.s << 32;
+    // Shift the pieces left by r = ce & 3 bytes (the loads started at the
+    // 4-byte aligned address below the chunk start); lane P's bytes continue
+    // in lane P+1 and, for lane 63, in its edge dword e[3].
+    const uint32_t r = (uint32_t)(ce & 3u);
+    if (M == kGeneral && c == 0 && cs > p) {
+      // Overhang: lane 0 turns the o = cs - p bytes before the chunk into a
+      // 16-byte piece ending at cs (bytes before p masked, ~init injected)
+      // from its edge load e[] = the 16 bytes below A4 (clamped up to p's
+      // granule g: moved up by qq dwords) and its first loaded dword (w[0]
+      // before the realign).  run_units prepends the four words to lane 0's
+      // chain; every other lane prepends zeros, which a zero register ignores.
+      const uintptr_t A4 = cs - r;
+      const uintptr_t g = p & ~(uintptr_t)15;
+      const uint32_t qq = A4 - 16u >= g ? 0u : (uint32_t)(g - (A4 - 16u)) >> 2;
+      uint32_t D[5];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int shk = rel - 4 * k;
-        const uint32_t keep = (uint32_t)(~0ull << (8 * min(max(shk, 0), 4)));
-        const uint32_t inj = (uint32_t)(s_hi >> ((32 - 8 * min(max(shk, -4), 4)) & 63));
-        w[k] = (w[k] & keep) ^ inj;
+      for (int k = 0; k < 4; ++k) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int m = 0; m <= k; ++m) v = (uint32_t)(k - m) == qq ? ch.e[m] : v;
+        D[k] = v;
       }
+      D[4] = w[0];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ov[k] = __builtin_amdgcn_alignbyte(D[k + 1], D[k], r);
+      mask_inject<4>(ov, (int)(int64_t)(p - (cs - 16u)), bi.s);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ov[k] = lane == 0 ? ov[k] : 0u;
+    }
+#if !defined(NVL_ABL_NOREALIGN)
+    if (r != 0) {
+      // lane 63's dword past the last piece: e[3], or -- a head chunk whose
+      // edge load was clamped up to p's granule g -- the dword at A4 + 4096
+      uint32_t last = ch.e[3];
+      if constexpr (M == kHead) {
+        const uintptr_t A4 = cs - r;
+        const uintptr_t g = p & ~(uintptr_t)15;
+        if (A4 + kChunk - 12u < g) {
+          const uint32_t x = (uint32_t)(A4 + kChunk - g) >> 2;  // 0..3, wave-uniform
+          last = x == 0 ? ch.e[0] : (x == 1 ? ch.e[1] : (x == 2 ? ch.e[2] : ch.e[3]));
+        }
+      }
+      const uint32_t nx = next_lane(w[0], last);
+#pragma unroll
+      for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+      w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
+    }
+#endif
+    if constexpr (M == kHead) {
+#if !defined(NVL_ABL_NOMASK)
+      // bytes before the start masked, ~init injected
+      mask_inject<16>(w, (int)(int64_t)(p - cs) - 64 * (int)opaque((uint32_t)lane), bi.s);
+#endif
+    } else if (c == 0 && cs < p + 4) {
+      // a chunk that starts at the buffer start, or 1..3 bytes after it (the
+      // overhang holds those bytes): ~init, or what the overhang leaves of it,
+      // goes into lane 0's first word
+      if (lane == 0) w[0] ^= bi.s >> (8u * (uint32_t)(cs - p));
     }
   }
+}
+
+// lane 0's chain over the overhang piece, folded into its first word: the
+// register the 16-word chain must start from (see build_words).
+__device__ __forceinline__ uint32_t overhang_start(const uint8_t* lds, const LaneBase& lb, const uint32_t (&ov)[4],
+                                                   uint32_t w0) {
+  uint32_t crc = ov[0];
+  crc = slice4_next(lds, crc, ov[1], lb);
+  crc = slice4_next(lds, crc, ov[2], lb);
+  crc = slice4_next(lds, crc, ov[3], lb);
+  return slice4_next(lds, crc, w0, lb);
 }
 
 // Serial slice-by-4 chains + butterflies of U chunks from their built words,
@@ -612,9 +727,9 @@ template <int M, int U>
 __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo (&bi)[U],
                                           const uint32_t (&c)[U], int lane, const Chunk (&ch)[U],
                                           uint32_t (&raw)[U]) {
-  uint32_t w[U][16];
+  uint32_t w[U][16], ov[4];
 #pragma unroll
-  for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u]);
+  for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u], ov);
   chains<U, false>(lds, lb, w, lane, raw);
 }
 
@@ -639,17 +754,6 @@ __device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase
   group_raw<M, 1>(lds, lb, b1, c1, lane, h1, r1);
   return r1[0];
 }
-
-// Buffers shorter than 4 bytes: bytewise (util/crc32c.cc:287 STEP1), lane-uniform.
-__device__ __forceinline__ uint32_t tiny_crc(const uint8_t* lds, const BufInfo& bi) {
-  uint32_t l = bi.s;  // = ~init
-  for (uint32_t k = 0; k < (uint32_t)bi.len; ++k) {
-    const uint32_t b = bi.p[k];
-    l = lds_u32(lds + kSliceOff, ((l ^ b) & 0xFFu) << 8) ^ (l >> 8);  // T0, replica 0
-  }
-  return ~l;
-}
-
 
 // Position of one chunk.
 struct Pos {
@@ -686,19 +790,35 @@ struct UnitState {
   Rec head;
 };
 
+// hx: the buffer's head contribution when this chunk is its last (kGeneral
+// with a partial first chunk, prefetched from KArgs::hc), else 0.
 __device__ __forceinline__ void consume(UnitState& st, const Pos& p, uint32_t raw, const uint8_t* lds, int lane,
-                                        const KArgs& ka) {
+                                        const KArgs& ka, uint32_t hx = 0u) {
   st.acc = st.cnt ? (shift4096(lds, st.acc, lane) ^ raw) : raw;
   ++st.cnt;
   if (p.c + 1 == p.bi.J) {
     if (st.from_zero) {
-      if (lane == 0) ka.out[p.i] = finish(~st.acc, ka.flags);
+      if (lane == 0) ka.out[p.i] = finish(~(st.acc ^ hx), ka.flags);
     } else {
       st.head = Rec{p.i, st.acc, st.cnt | kRecEnds};
     }
     st.cnt = 0;
     st.from_zero = true;
   }
+}
+
+// A portion's raw register normalized to the end of its buffer:
+// shift(acc, 4096 * after), `after` = chunks of the buffer after the portion.
+// Every record then combines by XOR alone (no serial walk of shifts in the
+// fix-up).  Few chunks: `after` shift4096 lookups; more: the GF(2) power
+// ladder over the x^(2^k) table.
+__device__ __forceinline__ uint32_t normalize(const uint8_t* lds, const uint32_t* tables, uint32_t acc,
+                                              uint32_t after, int lane) {
+  if (after <= 24) {
+    for (uint32_t k = 0; k < after; ++k) acc = shift4096(lds, acc, lane);
+    return acc;
+  }
+  return nvl::shift_bytes(tables + kGX2n, acc, (uint64_t)after * kChunk);
 }
 
 __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane) {
@@ -848,11 +968,22 @@ template <int M, int NW, class G>
 __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   constexpr int kStep = M == kAligned ? NVL_UNIT_STEP_ALIGNED : NVL_UNIT_STEP;
+  static_assert(M == kAligned || kStep == 1, "the kGeneral loop skips head chunks one step at a time");
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t T = g.total();
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
   auto lo_of = [&](uint32_t uu) -> uint64_t { return g.unit_lo(T, uu); };
+  // kGeneral: a head chunk (partial first chunk, or a buffer of < 4 bytes)
+  // belongs to crc32c_head_kernel: the step that reaches one loads and
+  // computes nothing; the buffer's other chunks add its contribution hc[i]
+  // when they complete it (prefetched with its last chunk, hv).
+  auto skip = [&](const Pos& q) -> bool { return M == kGeneral && q.c == 0 && head_first(q.bi.len); };
+  auto first_body = [&](const Pos& q) -> uint32_t { return (M == kGeneral && head_first(q.bi.len)) ? 1u : 0u; };
+  auto hc_of = [&](const Pos& q) -> uint32_t {  // vector load, in vmcnt order behind the chunk's own loads
+    if (M != kGeneral || !ka.hc || q.c + 1 != q.bi.J || !head_first(q.bi.len)) return 0u;
+    return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)(ka.hc + q.i));
+  };
 
   // One flat loop over steps.  A step is the next two chunks of the current
   // unit u (one at an odd tail; none when u is empty), their chains
@@ -865,9 +996,11 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   uint64_t t = lo_of(u), t1 = lo_of(u + 1);
   Pos p0{}, p1{};
   Chunk c0, c1;
+  uint32_t hv0 = 0u;
   if (t < t1) {  // the first step's loads overlap the LDS fill
     p0 = unit_start_pos(g, u, t);
-    load_chunk<M>(p0.bi, p0.c, lane, c0);
+    if (!skip(p0)) load_chunk<M>(p0.bi, p0.c, lane, c0);
+    hv0 = hc_of(p0);
     if (kStep == 2 && t + 1 < t1) {
       p1 = next_pos(g, p0);
       load_chunk<M>(p1.bi, p1.c, lane, c1);
@@ -880,7 +1013,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
 
   uint32_t un = ub0 + pull_unit(lds, lane);
   uint64_t un_lo = un < ub1 ? lo_of(un) : 0, un_hi = un < ub1 ? lo_of(un + 1) : 0;
-  UnitState st{0u, 0u, p0.c == 0, Rec{kNoBuf, 0u, 0u}};
+  UnitState st{0u, 0u, p0.c <= first_body(p0), Rec{kNoBuf, 0u, 0u}};
   Rec tail{kNoBuf, 0u, 0u};
   while (true) {
     const bool cur = t < t1;
@@ -904,36 +1037,41 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
         q1v = true;
       }
     }
+    const bool work = cur && !skip(p0);
     // Build the words first (c0/c1 die), then put the next step's loads in
     // flight, then run the chains.
     uint32_t w[2][16];
-    if (cur) {
-      build_words<M>(p0.bi, p0.c, lane, c0, w[0]);
-      if (two) build_words<M>(p1.bi, p1.c, lane, c1, w[1]);
+    uint32_t ov[2][4];
+    if (work) {
+      build_words<M>(p0.bi, p0.c, lane, c0, w[0], ov[0]);
+      if (two) build_words<M>(p1.bi, p1.c, lane, c1, w[1], ov[1]);
     }
     Chunk n0, n1;
-    if (q0v) load_chunk<M>(q0.bi, q0.c, lane, n0);
+    uint32_t hvn = 0u;
+    if (q0v && !skip(q0)) load_chunk<M>(q0.bi, q0.c, lane, n0);
+    if (q0v) hvn = hc_of(q0);
     if (q1v) load_chunk<M>(q1.bi, q1.c, lane, n1);
-    if (cur) {
+    if (work) {
       NVL_COUNT();
+      if (M == kGeneral) {  // a first chunk with an overhang: lane 0's chain starts 16 bytes early
+        if (p0.c == 0 && chunk_end(p0.bi, 0) - kChunk > (uintptr_t)p0.bi.p)
+          w[0][0] = overhang_start(lds, lb, ov[0], w[0][0]);
+      }
       uint32_t r[2];
       if (two) {
         chains<2, false>(lds, lb, w, lane, r);
       } else {
         r[0] = chain_fold<M>(lds, lb, w[0], lane);
       }
-      if (M == kGeneral) {  // buffers of < 4 bytes: bytewise, replacing the (unused) chain
-        if (p0.bi.len < 4) r[0] = ~tiny_crc(lds, p0.bi);
-        if (two && p1.bi.len < 4) r[1] = ~tiny_crc(lds, p1.bi);
-      }
-      consume(st, p0, r[0], lds, lane, ka);
+      consume(st, p0, r[0], lds, lane, ka, hv0);
       if (two) consume(st, p1, r[1], lds, lane, ka);
     }
     if (unit_ends) {
-      if (st.cnt) {
-        const uint64_t last_i = two ? p1.i : p0.i;  // buffer of the step's last chunk
-        if (st.from_zero) tail = Rec{last_i, st.acc, st.cnt};
-        else st.head = Rec{last_i, st.acc, st.cnt};
+      if (st.cnt) {  // the unit ends inside a buffer: its portion, normalized to the buffer end
+        const Pos& pl = two ? p1 : p0;  // the step's last chunk
+        const uint32_t norm = normalize(lds, ka.tables, st.acc, pl.bi.J - 1u - pl.c, lane);
+        if (st.from_zero) tail = Rec{pl.i, norm, st.cnt};
+        else st.head = Rec{pl.i, norm, st.cnt};
       }
       if (lane == 0) g.put_recs(ka, lds, u, st.head, tail);
       if (un >= ub1) break;
@@ -943,7 +1081,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
       un = ub0 + pull_unit(lds, lane);
       un_lo = un < ub1 ? lo_of(un) : 0;
       un_hi = un < ub1 ? lo_of(un + 1) : 0;
-      st = UnitState{0u, 0u, q0.c == 0, Rec{kNoBuf, 0u, 0u}};
+      st = UnitState{0u, 0u, q0.c <= first_body(q0), Rec{kNoBuf, 0u, 0u}};
       tail = Rec{kNoBuf, 0u, 0u};
     } else {
       t = tn;
@@ -952,8 +1090,143 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
     p1 = q1;
     c0 = n0;
     c1 = n1;
+    hv0 = hvn;
   }
   NVL_STAMP_END();
+}
+
+// ---------------------------------------------------------------------------
+// Head chunks -- crc32c_head_kernel, launched before the kGeneral body
+// kernel of the same batch.  Workgroup b owns buffers [n*b/G, n*(b+1)/G) and
+// takes them kHeadBatch at a time in two phases:
+//   1. classify, lane-parallel (each lane one buffer; waves take groups of
+//      64): a buffer of < 4 bytes is finished bytewise by its lane
+//      (util/crc32c.cc:287 STEP1 semantics), one without a head chunk gets
+//      hc[i] = 0, one with a partial first chunk is appended to an LDS list;
+//   2. the waves pull list items one at a time, each a masked chunk pass, the
+//      next item's chunk loads and the one after's metadata (vector loads, so
+//      nothing in flight couples with the chains' LDS waits) issued before
+//      the current item computes.  A one-chunk buffer is finished (out[i]),
+//      a longer one leaves hc[i] = its head normalized to the buffer end.
+constexpr uint32_t kHeadBatch = 960;                        // list capacity (u32 items)
+constexpr uint32_t kHeadListOff = kLdsBytes;                // after the table image
+constexpr uint32_t kHeadCtrOff = kHeadListOff + 4u * kHeadBatch;  // u32 list_n, queue
+constexpr uint32_t kHeadLdsBytes = kHeadCtrOff + 16u;
+static_assert(kHeadLdsBytes <= 160u * 1024u, "head kernel LDS exceeds 160 KiB");
+
+struct ItemMeta {  // one item's metadata as vector loads (every lane the same address)
+  uintptr_t p;
+  uint64_t L;
+  uint32_t s;
+};
+
+template <class G>
+__device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t n = g.n;
+  const uint64_t B0 = n * blockIdx.x / gridDim.x, B1 = n * (blockIdx.x + 1) / gridDim.x;
+  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kHeadListOff);
+  uint32_t* list_n = reinterpret_cast<uint32_t*>(lds + kHeadCtrOff);
+  uint32_t* queue = list_n + 1;
+  fill_lds<kWavesPerWG>(lds, ka.tables);
+  const LaneBase lb = make_lane_base(lane);
+  for (uint64_t s0 = B0; s0 < B1; s0 += kHeadBatch) {
+    const uint32_t nb = (uint32_t)min((uint64_t)kHeadBatch, B1 - s0);
+    if (threadIdx.x == 0) {
+      *list_n = 0u;
+      *queue = 0u;
+    }
+    __syncthreads();  // (also: the table image is complete)
+    for (uint32_t grp = wv; grp * kWave < nb; grp += kWavesPerWG) {
+      const uint32_t li = grp * kWave + (uint32_t)lane;
+      const uint64_t i = s0 + li;
+      const bool valid = li < nb;
+      uintptr_t lp = 0;
+      uint64_t lL = 0;
+      uint32_t ls = 0;
+      if (valid) g.lane_meta(i, lp, lL, ls);
+      const bool tiny = valid && lL < 4;
+      const bool head = valid && !tiny && head_first(lL);
+      if (tiny) {
+        uint32_t l = ls;  // = ~init
+        for (uint32_t k = 0; k < (uint32_t)lL; ++k) {
+          const uint32_t b = reinterpret_cast<const uint8_t*>(lp)[k];
+          l = lds_u32(lds + kSliceOff, (((l ^ b) & 0xFFu) << 8) | ((uint32_t)(lane & 31) << 2)) ^ (l >> 8);  // T0
+        }
+        ka.out[i] = finish(~l, ka.flags);
+      } else if (valid && !head && ka.hc) {
+        ka.hc[i] = 0u;
+      }
+      const uint64_t m = __ballot(head);
+      uint32_t base = 0;
+      if (lane == 0 && m)
+        base = __hip_atomic_fetch_add(list_n, (uint32_t)__builtin_popcountll(m), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (head) list[base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = li;
+    }
+    __syncthreads();
+    const uint32_t nitems = *list_n;
+    auto pull = [&]() -> uint32_t {
+      uint32_t v = 0;
+      if (lane == 0) v = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+    auto meta_load = [&](uint32_t k, ItemMeta& im) {
+      if (k < nitems) g.lane_meta(s0 + list[k], im.p, im.L, im.s);
+    };
+    auto info_of = [&](const ItemMeta& im) -> BufInfo {
+      const uint64_t L = uniform_u64(im.L);
+      return BufInfo{reinterpret_cast<const uint8_t*>(uniform_u64(im.p)), L, chunks_for(L), uniform_u32(im.s)};
+    };
+    uint32_t k = pull();
+    if (k < nitems) {
+      ItemMeta mc{}, mn{};
+      meta_load(k, mc);
+      BufInfo bi = info_of(mc);
+      Chunk cur;
+      load_chunk<kHead>(bi, 0, lane, cur);
+      uint32_t kn = pull();
+      meta_load(kn, mn);
+      while (true) {
+        uint32_t w[16], ov[4];
+        build_words<kHead>(bi, 0, lane, cur, w, ov);
+        const bool more = kn < nitems;
+        BufInfo bn = bi;
+        Chunk nxt;
+        uint32_t knn = nitems;
+        ItemMeta mnn{};
+        if (more) {
+          bn = info_of(mn);
+          load_chunk<kHead>(bn, 0, lane, nxt);
+          knn = pull();
+          meta_load(knn, mnn);
+        }
+        const uint32_t raw = chain_fold<kHead>(lds, lb, w, lane);
+        const uint64_t ib = s0 + list[k];
+        if (bi.J == 1) {
+          if (lane == 0) ka.out[ib] = finish(~raw, ka.flags);
+        } else {
+          const uint32_t nv = normalize(lds, ka.tables, raw, bi.J - 1u, lane);
+          if (lane == 0) ka.hc[ib] = nv;
+        }
+        if (!more) break;
+        k = kn;
+        kn = knn;
+        bi = bn;
+        mn = mnn;
+        cur = nxt;
+      }
+    }
+    __syncthreads();  // the list is reused by the next batch
+  }
+}
+
+template <class G>
+__global__ __launch_bounds__(kThreads, 1) void crc32c_head_kernel(G g, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLdsBytes];
+  run_heads(g, ka, lds);
 }
 
 #ifndef NVL_FAST_U
@@ -993,8 +1266,7 @@ __global__ void crc32c_var_counts(const uint64_t* __restrict__ lengths, uint64_t
                                   uint64_t* __restrict__ cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const uint64_t L = lengths[i];
-    cnt[i] = L <= kChunk ? 1u : (L + kChunk - 1) / kChunk;
+    cnt[i] = chunks_for(lengths[i]);
   } else if (i == n) {
     cnt[i] = 0;
   }
@@ -1053,7 +1325,7 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = t + (uint32_t)k * (uint32_t)kPlanThreads;
-      if (i < nn) js[plan_pad(i)] = Ls[k] <= kChunk ? 1u : (uint32_t)((Ls[k] + kChunk - 1) / kChunk);
+      if (i < nn) js[plan_pad(i)] = chunks_for(Ls[k]);
     }
   }
   __syncthreads();
@@ -1100,42 +1372,41 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t
   }
 }
 
-// Fold the per-unit records of buffers cut by work-unit boundaries: unit w's
-// head record, if it holds the LAST portion of a buffer, walks back over
-// earlier units for the buffer's other portions.
-__device__ __forceinline__ void fixup_unit(const Rec* __restrict__ recs, uint32_t w, const uint32_t* __restrict__ tables,
-                                           uint32_t* __restrict__ out, uint32_t flags) {
-  const Rec h = recs[2 * w];
+// Fold the per-unit records of buffers cut by work-unit boundaries.  Records
+// are normalized (each portion already shifted to its buffer's end), so a
+// buffer's CRC is the XOR of its portions: unit w's head record, when it
+// holds the LAST portion, plus the head records (middle portions) and the
+// tail record (first portion) of the units before it; units with an empty
+// chunk range carry no records.  One wave per unit w walks back 64 units per
+// step (one record pair per lane), so a buffer spanning thousands of units
+// costs tens of steps, not thousands of serial ones.
+__global__ __launch_bounds__(256) void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
+                                                           uint32_t* __restrict__ out, uint32_t flags,
+                                                           const uint32_t* __restrict__ hc) {
+  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  if (w >= nw) return;
+  const Rec h = recs[2 * (uint64_t)w];
   if (h.buf == kNoBuf || !(h.cnt & kRecEnds)) return;
-  const uint32_t* x2n = tables + kGX2n;
-  uint32_t total = h.raw;
-  uint64_t after = h.cnt & ~kRecEnds;  // chunks after the current portion
-  // Units between the buffer's first and last portion either hold a middle
-  // portion (head record of this buffer) or have an empty chunk range (no
-  // records); the first portion is the tail record of an earlier unit.
-  for (int64_t x = (int64_t)w - 1; x >= 0; --x) {
-    const Rec hx = recs[2 * x];
-    if (hx.buf == h.buf) {  // a middle portion
-      total ^= nvl::shift_bytes(x2n, hx.raw, after * kChunk);
-      after += hx.cnt & ~kRecEnds;
-      continue;
+  uint32_t acc = lane == 0 ? h.raw : 0u;
+  for (int64_t base = (int64_t)w - 1; base >= 0; base -= kWave) {
+    const int64_t x = base - lane;
+    Rec hx{kNoBuf, 0u, 0u}, tx{kNoBuf, 0u, 0u};
+    if (x >= 0) {
+      hx = recs[2 * x];
+      tx = recs[2 * x + 1];
     }
-    const Rec tx = recs[2 * x + 1];
-    if (tx.buf == h.buf) {  // the first portion
-      total ^= nvl::shift_bytes(x2n, tx.raw, after * kChunk);
-      break;
-    }
-    if (hx.buf != kNoBuf || tx.buf != kNoBuf) break;  // unreachable for a consistent plan
+    const bool mid = hx.buf == h.buf;                  // a middle portion
+    const bool first = !mid && tx.buf == h.buf;        // the first portion: the walk ends here
+    const bool other = !mid && !first && (hx.buf != kNoBuf || tx.buf != kNoBuf || x < 0);
+    const unsigned long long stop = __ballot(first || other);
+    const int lim = stop ? __builtin_ctzll(stop) : kWave;  // lanes below lim: middle or empty units
+    if ((lane < lim && mid) || (lane == lim && first)) acc ^= lane < lim ? hx.raw : tx.raw;
+    if (stop) break;
   }
-  out[h.buf] = finish(~total, flags);
-}
-
-// One thread per unit.
-__global__ void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
-                                    const uint32_t* __restrict__ tables, uint32_t* __restrict__ out,
-                                    uint32_t flags) {
-  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < nw) fixup_unit(recs, w, tables, out, flags);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+  if (lane == 0) out[h.buf] = finish(~(acc ^ (hc ? hc[h.buf] : 0u)), flags);
 }
 
 // ---------------------------------------------------------------------------
@@ -1191,9 +1462,8 @@ struct VarGeomFused {
   }
   __device__ __forceinline__ BufInfo info(uint64_t i) const {
     const uint64_t L = ldc(lengths, i);
-    const uint32_t J = L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
     const uint32_t ini = init ? ldc(init, i) : init_all;
-    return BufInfo{base + ldc(offsets, i), L, J, ~ini};
+    return BufInfo{base + ldc(offsets, i), L, chunks_for(L), ~ini};
   }
   __device__ __forceinline__ void put_recs(const KArgs&, uint8_t* lds, uint32_t u, const Rec& h, const Rec& t) const {
     Rec* r = reinterpret_cast<Rec*>(lds + kRecOff);
@@ -1212,16 +1482,11 @@ __device__ unsigned long long g_fstamps[8 * 1024];
 
 // Plan prologue.  After it: LDS holds ubuf/uc for the 64 local units, and
 // C0/C1 (returned) bound the workgroup's chunk range.
-__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-         __builtin_amdgcn_readfirstlane((uint32_t)v);
-}
-
 template <int NW>
 __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restrict__ lengths, uint32_t nn,
                                            uint64_t& C0, uint64_t& C1) {
   constexpr uint32_t kT = kWave * NW;
-  static_assert(kT == 1024, "plan layout assumes 1024 threads");
+  static_assert(kT <= 1024 && kPlanSmallMax % kT == 0, "plan layout assumes <= 1024 threads");
   constexpr int kPer = (int)(kPlanSmallMax / kT);
   uint32_t* js = reinterpret_cast<uint32_t*>(lds);
   uint64_t* wsum = reinterpret_cast<uint64_t*>(lds + kPlanWsumOff);
@@ -1239,7 +1504,7 @@ __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restr
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = t + (uint32_t)k * kT;
-      if (i < nn) js[plan_pad(i)] = Ls[k] <= kChunk ? 1u : (uint32_t)((Ls[k] + kChunk - 1) / kChunk);
+      if (i < nn) js[plan_pad(i)] = chunks_for(Ls[k]);
     }
   }
   __syncthreads();
@@ -1305,22 +1570,19 @@ __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restr
   __syncthreads();
 }
 
-// Fold the earlier portions of buffer `buf` (LDS records of units x < k)
-// into (total, after): middle portions are head records, the first portion a
+// XOR into `total` the earlier portions of buffer `buf` (LDS records of units
+// x < k, normalized): middle portions are head records, the first portion a
 // tail record.  True when the first portion is in this workgroup.
-__device__ __forceinline__ bool fold_back(const Rec* lr, int k, unsigned long long buf, uint32_t& total,
-                                          uint64_t& after, const uint32_t* x2n) {
+__device__ __forceinline__ bool fold_back(const Rec* lr, int k, unsigned long long buf, uint32_t& total) {
   for (int x = k - 1; x >= 0; --x) {
     const Rec hx = lr[2 * x];
     if (hx.buf == buf) {
-      total ^= nvl::shift_bytes(x2n, hx.raw, after * kChunk);
-      after += hx.cnt & ~kRecEnds;
+      total ^= hx.raw;
       continue;
     }
     const Rec tx = lr[2 * x + 1];
     if (tx.buf == buf) {
-      total ^= nvl::shift_bytes(x2n, tx.raw, after * kChunk);
-      after += tx.cnt;
+      total ^= tx.raw;
       return true;
     }
     if (hx.buf != kNoBuf || tx.buf != kNoBuf) return false;  // unreachable for a consistent plan
@@ -1360,7 +1622,6 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
                        ubuf + kUnitsPerWG, ub0};
   run_units<kGeneral, kGenWaves>(g, ka, lds);
   NVL_FSTAMP(2);
-  const uint32_t* x2n = ka.tables + kGX2n;
   const Rec* lr = reinterpret_cast<const Rec*>(lds + kRecOff);
   Rec* edge = reinterpret_cast<Rec*>(lds + kEdgeOff);
   uint32_t* last = reinterpret_cast<uint32_t*>(lds + kEdgeOff + 2u * sizeof(Rec));
@@ -1371,9 +1632,8 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     const Rec h = lr[2 * t];
     if (h.buf != kNoBuf && (h.cnt & kRecEnds)) {
       uint32_t total = h.raw;
-      uint64_t after = h.cnt & ~kRecEnds;
-      if (fold_back(lr, (int)t, h.buf, total, after, x2n)) ka.out[h.buf] = finish(~total, ka.flags);
-      else edge[0] = Rec{h.buf, total, (uint32_t)after | kRecEnds};  // began before C0
+      if (fold_back(lr, (int)t, h.buf, total)) ka.out[h.buf] = finish(~(total ^ (ka.hc ? ka.hc[h.buf] : 0u)), ka.flags);
+      else edge[0] = Rec{h.buf, total, kRecEnds};  // began before C0
     }
   } else if (t == kUnitsPerWG) {  // the buffer of the range's last chunk, if it runs past C1
     int L = (int)kUnitsPerWG - 1;
@@ -1384,9 +1644,8 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
         edge[1] = tl;
       } else if (!(h.cnt & kRecEnds)) {  // a middle portion: the buffer covers unit L
         uint32_t total = h.raw;
-        uint64_t after = h.cnt;
-        if (fold_back(lr, L, h.buf, total, after, x2n)) edge[1] = Rec{h.buf, total, (uint32_t)after};
-        else edge[0] = Rec{h.buf, total, (uint32_t)after};  // began before C0 and runs past C1
+        if (fold_back(lr, L, h.buf, total)) edge[1] = Rec{h.buf, total, 0u};
+        else edge[0] = Rec{h.buf, total, 0u};  // began before C0 and runs past C1
       }
     }
   }
@@ -1403,8 +1662,8 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   NVL_FSTAMP(3);
   if (!*last) return;
   // The last workgroup: every edge record (sc1 loads) into the now free table
-  // image, then one thread per workgroup whose E_in ends a buffer folds it
-  // back through the earlier workgroups' edge records.
+  // image, then one thread per workgroup whose E_in ends a buffer XORs in the
+  // earlier workgroups' (normalized) edge records of that buffer.
   const uint32_t G = gridDim.x;
   Rec* E = reinterpret_cast<Rec*>(lds);  // [2b] = E_in of workgroup b, [2b+1] = E_out
   gu64* eg = (gu64*)ka.recs;
@@ -1414,21 +1673,19 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     const Rec e = E[2 * b];
     if (e.buf == kNoBuf || !(e.cnt & kRecEnds)) continue;
     uint32_t total = e.raw;
-    uint64_t after = e.cnt & ~kRecEnds;
     for (int bb = (int)b - 1; bb >= 0; --bb) {
       const Rec ei = E[2 * bb], eo = E[2 * bb + 1];
       if (ei.buf == e.buf) {  // a workgroup wholly inside the buffer
-        total ^= nvl::shift_bytes(x2n, ei.raw, after * kChunk);
-        after += ei.cnt;
+        total ^= ei.raw;
         continue;
       }
       if (eo.buf == e.buf) {  // the workgroup where it began
-        total ^= nvl::shift_bytes(x2n, eo.raw, after * kChunk);
+        total ^= eo.raw;
         break;
       }
       if (ei.buf != kNoBuf || eo.buf != kNoBuf) break;  // unreachable for a consistent plan
     }
-    ka.out[e.buf] = finish(~total, ka.flags);
+    ka.out[e.buf] = finish(~(total ^ (ka.hc ? ka.hc[e.buf] : 0u)), ka.flags);
   }
   if (t == 0) (void)__hip_atomic_exchange((gu32*)ka.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   NVL_FSTAMP(7);
@@ -1464,15 +1721,15 @@ hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64
   return hipGetLastError();
 }
 
-static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, const uint32_t* tables,
-                                      uint32_t* out, uint32_t flags, hipStream_t st, hipEvent_t ev_stop = nullptr) {
-  const uint32_t tpb = 256;
+static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, uint32_t* out, uint32_t flags, const uint32_t* hc,
+                                      hipStream_t st, hipEvent_t ev_stop = nullptr) {
+  const uint32_t wpb = 4;  // one wave per unit
+  const dim3 grid((nw + wpb - 1) / wpb), block(dev::kWave * wpb);
   if (ev_stop)
-    hipExtLaunchKernelGGL(dev::crc32c_fixup_kernel, dim3((nw + tpb - 1) / tpb), dim3(tpb), 0, st, nullptr, ev_stop,
-                          0u, recs, nw, tables, out, flags);
+    hipExtLaunchKernelGGL(dev::crc32c_fixup_kernel, grid, block, 0, st, nullptr, ev_stop, 0u, recs, nw, out, flags,
+                          hc);
   else
-    hipLaunchKernelGGL(dev::crc32c_fixup_kernel, dim3((nw + tpb - 1) / tpb), dim3(tpb), 0, st, recs, nw,
-                       tables, out, flags);
+    hipLaunchKernelGGL(dev::crc32c_fixup_kernel, grid, block, 0, st, recs, nw, out, flags, hc);
   return hipGetLastError();
 }
 
@@ -1482,43 +1739,81 @@ static inline uint32_t grid_for(int num_cu, uint64_t T) {
   return g ? (uint32_t)g : 1u;
 }
 
-static inline uint32_t chunks_of(uint64_t len) {
-  return len <= dev::kChunk ? 1u : (uint32_t)((len + dev::kChunk - 1) / dev::kChunk);
+static inline uint32_t chunks_of(uint64_t len) { return dev::chunks_for(len); }
+
+// The head kernel over a geometry's n buffers; its dispatch records
+// ev_start when given (it is then the call's first kernel).
+template <class G>
+static hipError_t launch_heads(const LaunchCtx& lc, const G& g, uint32_t* out, uint32_t flags, uint32_t* hc,
+                               hipEvent_t ev_start) {
+  const uint64_t groups = (g.n + dev::kWave - 1) / dev::kWave;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)lc.num_cu, groups));
+  const dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, hc};
+  if (ev_start)
+    hipExtLaunchKernelGGL(dev::crc32c_head_kernel<G>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, ev_start,
+                          nullptr, 0u, g, ka);
+  else
+    hipLaunchKernelGGL(dev::crc32c_head_kernel<G>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  return hipGetLastError();
+}
+
+static inline size_t recs_part(int num_cu, uint64_t len, uint64_t n) {
+  if (n == 0 || chunks_of(len) == 1) return 0;
+  return 2ull * grid_for(num_cu, n * (uint64_t)chunks_of(len)) * dev::kUnitsPerWG * sizeof(Rec);
+}
+
+// Fixed-stride workspace: [unit records (J > 1)][hc: n u32 (partial first chunks with J > 1)]
+size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
+  const size_t r = (recs_part(num_cu, len, n) + 255) / 256 * 256;
+  const bool hcs = n && chunks_of(len) > 1 && dev::head_first(len);
+  return r + (hcs ? n * sizeof(uint32_t) : 0);
 }
 
 hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
-                        const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs) {
+                        const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* ws) {
   if (n == 0) return hipSuccess;
   const uint32_t J = chunks_of(len);
   const uint32_t grid = grid_for(lc.num_cu, n * (uint64_t)J);
   const bool aligned = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
-  dev::KArgs ka{out, flags, J > 1 ? recs : nullptr, lc.tables, nullptr};
+  Rec* recs = J > 1 ? ws : nullptr;
+  const bool heads = !aligned && dev::head_first(len);  // every buffer's first chunk is a head chunk
+  const bool body = !(heads && J == 1);                 // some buffer has a full chunk
+  uint32_t* hc = heads && J > 1
+                     ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws) +
+                                                   (recs_part(lc.num_cu, len, n) + 255) / 256 * 256)
+                     : nullptr;
+  hipEvent_t ev_start = lc.ev_start;
+  if (heads) {
+    hipError_t eh = launch_heads(lc, g, out, flags, hc, ev_start);
+    if (eh != hipSuccess) return eh;
+    ev_start = nullptr;
+    if (!body) {
+      if (lc.ev_stop) return hipEventRecord(lc.ev_stop, lc.stream);
+      return hipSuccess;
+    }
+  }
+  dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc};
   hipEvent_t stop_main = J == 1 ? lc.ev_stop : nullptr;  // else the fix-up records it
-  const bool timed = lc.ev_start || stop_main;
+  const bool timed = ev_start || stop_main;
   if (aligned) {
     if (timed)
       hipExtLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream,
-                            lc.ev_start, stop_main, 0u, g, ka);
+                            ev_start, stop_main, 0u, g, ka);
     else
       hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g,
                          ka);
   } else {
     if (timed)
       hipExtLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kWave * dev::kGenWaves),
-                            0, lc.stream, lc.ev_start, stop_main, 0u, g, ka);
+                            0, lc.stream, ev_start, stop_main, 0u, g, ka);
     else
       hipLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kGeneral>, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0,
                          lc.stream, g, ka);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || J == 1) return e;
-  return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream, lc.ev_stop);
-}
-
-size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
-  if (n == 0 || chunks_of(len) == 1) return 0;
-  return 2ull * grid_for(num_cu, n * (uint64_t)chunks_of(len)) * dev::kUnitsPerWG * sizeof(Rec);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, hc, lc.stream, lc.ev_stop);
 }
 
 size_t var_recs_bytes(int num_cu) { return 2ull * (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(Rec); }
@@ -1539,11 +1834,13 @@ bool var_plan_small(uint64_t n) { return n <= dev::kPlanSmallMax; }
 
 hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                             uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
-                            Rec* recs) {
+                            Rec* recs, uint32_t* hc) {
   if (n == 0) return hipSuccess;
   if (n > dev::kPlanSmallMax || !lc.counter || lc.num_cu > (int)dev::kMaxFusedGrid) return hipErrorInvalidValue;
   dev::VarGeom g{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
-  dev::KArgs ka{out, flags, recs, lc.tables, lc.counter};
+  hipError_t eh = launch_heads(lc, g, out, flags, hc, nullptr);
+  if (eh != hipSuccess) return eh;
+  dev::KArgs ka{out, flags, recs, lc.tables, lc.counter, hc};
   hipLaunchKernelGGL(dev::crc32c_var_fused_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kWave * dev::kGenWaves), 0,
                      lc.stream, g, ka);
   return hipGetLastError();
@@ -1566,8 +1863,13 @@ hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt,
 
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
-                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, bool have_unit_map) {
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, bool have_unit_map) {
   if (n == 0) return hipSuccess;
+  {
+    const dev::VarGeom gh{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
+    hipError_t eh = launch_heads(lc, gh, out, flags, hc, nullptr);
+    if (eh != hipSuccess) return eh;
+  }
   const uint32_t grid = (uint32_t)lc.num_cu;  // chunk count is only known on the device
   const uint64_t NU = (uint64_t)grid * dev::kUnitsPerWG;
   if (!have_unit_map) {
@@ -1577,11 +1879,11 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
     if (e0 != hipSuccess) return e0;
   }
   dev::VarGeom g{base, offsets, lengths, chunk_start, unit_first, n, init, init_all};
-  dev::KArgs ka{out, flags, recs, lc.tables, nullptr};
+  dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc};
   hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0, lc.stream, g, ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_fixup(recs, grid * dev::kUnitsPerWG, lc.tables, out, flags, lc.stream);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, hc, lc.stream);
 }
 
 }  // namespace nvl

@@ -99,43 +99,100 @@ def wave_fold(g):
     return g[0]
 
 
+OVER = 16  # overhang: a first chunk of up to 4096 + OVER bytes is ONE pass
+
+
+def chunks_of(L: int) -> int:
+    """Chunks of a buffer of L bytes (crc32c_kernels.hip chunks_for): END-aligned
+    4096-byte chunks; a first chunk of 4097..4096+OVER bytes is not split."""
+    return 1 if L <= CHUNK + OVER else (L - OVER + CHUNK - 1) // CHUNK
+
+
+def _mask_inject(words, rel: int, s: int):
+    """Zero the bytes of a piece before the buffer start (rel = bytes of the
+    piece before it) and XOR ~init (s) into the 4 bytes at the start."""
+    rel = max(-8, min(72, rel))
+    out = []
+    for k, w in enumerate(words):
+        sh = rel - 4 * k
+        keep = 0xFFFFFFFF if sh <= 0 else (0 if sh >= 4 else (0xFFFFFFFF << (8 * sh)) & 0xFFFFFFFF)
+        inj = 0
+        if 0 <= sh < 4:
+            inj = (s << (8 * sh)) & 0xFFFFFFFF
+        elif -4 < sh < 0:
+            inj = s >> (-8 * sh)
+        out.append((w & keep) ^ inj)
+    return out
+
+
 def chunk_raw(mem: bytes, p: int, L: int, J: int, c: int, s: int) -> int:
-    """Raw register of chunk c of buffer [p, p+L) with ~init = s injected."""
-    ce = p + L - CHUNK * (J - 1 - c)
-    m = ce & 15
+    """Raw register of chunk c of buffer [p, p+L) with ~init = s injected,
+    computed the way load_chunk<kGeneral> / build_words<kGeneral> do it."""
+    e = p + L
+    ce = e - CHUNK * (J - 1 - c)
+    cs = ce - CHUNK
+    r = ce & 3
+    A4 = cs - r  # every chunk is loaded from the 4-byte aligned address below its start
+    g = p & ~15
+    head = cs < p
+
+    def load(a: int, n: int) -> bytes:
+        # fault safety: only 16-B granules that hold buffer bytes are touched
+        assert (a & ~15) >= g and ((a + n - 1) & ~15) <= ((e - 1) & ~15), (a, n, p, e)
+        return mem[a:a + n]
+
+    slots = bytearray(CHUNK + 4)
+    for k in range(CHUNK // 16):
+        a = A4 + 16 * k
+        if head and a + 16 <= g:
+            continue  # wholly before the granule of p: not loaded (zeros)
+        if head and a < g:
+            d = load(g, 16)  # clamped to p's granule, then moved up by g - a bytes
+            slots[16 * k + (g - a):16 * k + 16] = d[:16 - (g - a)]
+        else:
+            slots[16 * k:16 * k + 16] = load(a, 16)
+    if r:  # lane 63's 16-byte edge load ending at A4 + 4100, clamped up to g (a short head's buffer)
+        ea = max(A4 + CHUNK - 12, g)
+        edge = load(ea, 16)
+        slots[CHUNK:CHUNK + 4] = edge[A4 + CHUNK - ea:A4 + CHUNK - ea + 4]
     lanes = []
     for lane in range(64):
-        ps = ce - 64 * (64 - lane)
-        a = ps - m
-        # load_piece<false>: 16-byte vectors, skipped when wholly before p;
-        # bytes of a loaded vector outside [p, e) are whatever memory holds.
-        d = bytearray(80)
-        for j in range(5):
-            if (j < 4 or m != 0) and a + 16 * j + 16 > p:
-                d[16 * j:16 * j + 16] = mem[a + 16 * j:a + 16 * j + 16]
-        words = [int.from_bytes(d[m + 4 * k:m + 4 * k + 4], "little") for k in range(16)]
-        if ce - CHUNK < p + 4:  # head: keep-mask bytes before p, inject ~init
-            rel = max(-8, min(72, p - ps))
-            for k in range(16):
-                sh = rel - 4 * k
-                keep = 0xFFFFFFFF if sh <= 0 else (0 if sh >= 4 else (0xFFFFFFFF << (8 * sh)) & 0xFFFFFFFF)
-                inj = 0
-                if 0 <= sh < 4:
-                    inj = (s << (8 * sh)) & 0xFFFFFFFF
-                elif -4 < sh < 0:
-                    inj = s >> (-8 * sh)
-                words[k] = (words[k] & keep) ^ inj
+        piece = slots[r + 64 * lane:r + 64 * lane + 64]  # bytes [cs + 64 lane, +64)
+        words = [int.from_bytes(piece[4 * k:4 * k + 4], "little") for k in range(16)]
+        if head:
+            words = _mask_inject(words, p - (cs + 64 * lane), s)
+        elif c == 0 and lane == 0 and p <= cs < p + 4:
+            words[0] ^= s >> (8 * (cs - p))  # ~init, or what the overhang leaves of it
         crc = 0
         for w in words:
             crc = slice4(crc ^ w)
         lanes.append(crc)
-    return wave_fold(lanes)
+    raw = wave_fold(lanes)
+    if c == 0 and cs > p:  # overhang: bytes [p, cs) as a 16-byte piece ending at cs
+        o = cs - p
+        assert 1 <= o <= OVER
+        r2 = cs & 3
+        B4 = cs - 16 - r2  # = A4 - 16
+        dw = bytearray(20)
+        ea = max(B4, g)  # lane 0's 16-byte edge load, clamped up to g
+        edge = load(ea, 16)
+        dw[ea - B4:16] = edge[:16 - (ea - B4)]
+        dw[16:20] = load(B4 + 16, 4)  # lane 0's first loaded dword (A4)
+        words = [int.from_bytes(dw[r2 + 4 * k:r2 + 4 * k + 4], "little") for k in range(4)]
+        words = _mask_inject(words, p - (cs - 16), s)
+        crc = 0
+        for w in words:
+            crc = slice4(crc ^ w)
+        raw ^= apply_op(SH4096, crc)
+    return raw
 
 
 def batch(mem: bytes, bufs, inits, nwaves: int):
-    """bufs: list of (p, L).  Returns final CRCs via waves + records + fix-up."""
+    """bufs: list of (p, L).  Returns final CRCs via waves + records + fix-up.
+    Records hold NORMALIZED portions: the portion's raw shifted to the end of
+    its buffer (4096 * chunks after it), so the fix-up only XORs."""
     n = len(bufs)
-    J = [1 if L <= CHUNK else (L + CHUNK - 1) // CHUNK for (_, L) in bufs]
+    J = [chunks_of(L) for (_, L) in bufs]
     cs = [0]
     for j in J:
         cs.append(cs[-1] + j)
@@ -145,7 +202,7 @@ def batch(mem: bytes, bufs, inits, nwaves: int):
     NOBUF = -1
     for w in range(nwaves):
         t0, t1 = Ttot * w // nwaves, Ttot * (w + 1) // nwaves
-        head, tail = (NOBUF, 0, 0, False), (NOBUF, 0, 0, False)
+        head, tail = (NOBUF, 0, False), (NOBUF, 0, False)
         if t0 < t1:
             i = max(k for k in range(n) if cs[k] <= t0)
             c = t0 - cs[i]
@@ -165,32 +222,32 @@ def batch(mem: bytes, bufs, inits, nwaves: int):
                         if from_zero:
                             out[i] = (~acc) & 0xFFFFFFFF
                         else:
-                            head = (i, acc, cnt, True)
+                            head = (i, acc, True)  # ends the buffer: already normalized
                         cnt, from_zero = 0, True
+                    elif t + 1 == t1:  # the unit ends inside buffer i, after its chunk c
+                        norm = shift(acc, CHUNK * (J[i] - 1 - c))
+                        if from_zero:
+                            tail = (i, norm, False)
+                        else:
+                            head = (i, norm, False)
                 if c + 1 == J[i]:
                     i, c = i + 1, 0
                 else:
                     c += 1
-            if cnt:
-                if from_zero:
-                    tail = (i, acc, cnt, False)
-                else:
-                    head = (i, acc, cnt, False)
         recs.append((head, tail))
-    # fix-up
+    # fix-up: XOR of the normalized portions
     for w in range(nwaves):
         h = recs[w][0]
-        if h[0] == NOBUF or not h[3]:
+        if h[0] == NOBUF or not h[2]:
             continue
-        total, after = h[1], h[2]
+        total = h[1]
         for x in range(w - 1, -1, -1):
             hx, tx = recs[x]
             if hx[0] == h[0]:  # middle portion
-                total ^= shift(hx[1], after * CHUNK)
-                after += hx[2]
+                total ^= hx[1]
                 continue
             if tx[0] == h[0]:  # first portion
-                total ^= shift(tx[1], after * CHUNK)
+                total ^= tx[1]
                 break
             assert hx[0] == NOBUF and tx[0] == NOBUF  # empty-range wave
         else:

@@ -41,7 +41,12 @@ def usage(tmp_path_factory):
 
 
 HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_var_kernel", "crc32c_var_fused_kernel",
-       "crc32c_plan_small", "crc32c_fixup_kernel"]
+       "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel"]
+# SGPR spills go to VGPR lanes (v_writelane/v_readlane), not memory: a bound
+# per kernel so that a jump shows.  The fused kernel parks plan-phase scalars
+# there; the head kernel keeps two items' metadata (current, next) live in
+# SGPRs while the next-but-one's loads are in flight.
+SGPR_SPILL_MAX = {"crc32c_var_fused_kernel": 32, "crc32c_head_kernel": 160}
 
 
 @pytest.mark.parametrize("name", HOT)
@@ -51,7 +56,5 @@ def test_no_vgpr_spills(usage, name):
     for k in hits:
         u = usage[k]
         assert u.get("VGPRs Spill", 0) == 0, (k, u)
-        # SGPR spills go to VGPR lanes (v_writelane/v_readlane), not memory;
-        # the fused kernel parks a few plan-phase scalars there.
-        assert u.get("SGPRs Spill", 0) <= 16, (k, u)
+        assert u.get("SGPRs Spill", 0) <= SGPR_SPILL_MAX.get(name, 16), (k, u)
         assert u.get("ScratchSize", 0) <= 32, (k, u)  # a small indexed private array, no spill area

@@ -92,7 +92,7 @@ def test_fast_path_transposed_fold(port):
     assert (~km.raw_bytes(0xFFFFFFFF, data)) & 0xFFFFFFFF == port.value(data)
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(24))
 def test_general_path_model(port, seed):
     """End-aligned chunks, masking, injection, per-wave ranges, records and
     fix-up, with more waves than chunks and buffers straddling waves."""
@@ -100,7 +100,8 @@ def test_general_path_model(port, seed):
     mem = bytes(port.fill(1000 + seed, 0, 120000))
     bufs, pos = [], 64
     for _ in range(rng.randrange(1, 7)):
-        L = rng.choice([0, 1, 2, 3, 4, 5, 17, 63, 64, 65, 4095, 4096, 4097, 8192, 9000, 13000, 20000])
+        L = rng.choice([0, 1, 2, 3, 4, 5, 17, 63, 64, 65, 4095, 4096, 4097, 4100, 4109, 4112, 4113, 8192, 8208,
+                        8209, 9000, 13000, 20000])
         pos += rng.randrange(0, 40)
         bufs.append((pos, L))
         pos += L
@@ -109,3 +110,23 @@ def test_general_path_model(port, seed):
     got = km.batch(mem, bufs, inits, nw)
     want = [port.extend(i, mem[a:a + L]) for (a, L), i in zip(bufs, inits)]
     assert got == want
+
+
+def test_overhang_alignment_sweep_model(port):
+    """Every start alignment mod 16 x lengths around the chunk and overhang
+    boundaries (4096, 4096 + OVER) through the model, with garbage before and
+    after each buffer; the model also asserts that no load touches a 16-byte
+    granule without buffer bytes (fault safety)."""
+    mem = bytes(port.fill(0xA11, 0, 140000))
+    lens = [4, 5, 6, 7, 15, 16, 17, 63, 64, 65, 4095, 4096, 4097, 4098, 4099, 4100, 4101, 4108, 4111, 4112,
+            4113, 4114, 8207, 8208, 8209, 8210, 8212]
+    for a in range(16):
+        bufs = []
+        pos = 4096 + a
+        for L in lens:
+            bufs.append((pos, L))
+            pos += L + 16 * 7 + 3
+        inits = [(0x1F2E3D4C * (k + 1) + a) & 0xFFFFFFFF for k in range(len(bufs))]
+        got = km.batch(mem, bufs, inits, 1)
+        want = [port.extend(i, mem[p:p + L]) for (p, L), i in zip(bufs, inits)]
+        assert got == want, a

@@ -1,5 +1,13 @@
-"""Time BASELINE configs 2-4 through the C ABI (HIP events, median of R reps).
-    python tools/bench_configs.py [--lib build/libnvl_crc32c_X.so] [--configs 2,3,4]"""
+"""Time BASELINE configs and the call-site shapes through the C ABI (HIP events
+around each call, median of R reps), every result checked.
+    python tools/bench_configs.py [--lib build/libnvl_crc32c_X.so] [--configs 2,3,4,v,g,r]
+  2, 3, 4  BASELINE configs 2-4 (golden digests)
+  v        10^5 x 4097 B at stride 4101: block | type of 4096-byte SSTable blocks with their
+           4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
+  g        10^5 x 4096 B at stride 4099 from an odd base: the fixed-stride general path
+  r        10^5 buffers of 3364..4109 B (the n+1 of data blocks at block_size 4096)
+           at stride length+4, nvl_crc32c_batch_dev
+v, g and r are checked CRC by CRC against the oracle."""
 import argparse, ctypes, json, os, sys
 import numpy as np, torch
 ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -22,6 +30,7 @@ st = torch.cuda.current_stream().cuda_stream
 g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
 p = oracle.port()
 
+
 def timeit(fn, reps):
     for _ in range(3): fn()
     torch.cuda.synchronize()
@@ -31,9 +40,23 @@ def timeit(fn, reps):
     torch.cuda.synchronize()
     return float(np.median([ev[2*j].elapsed_time(ev[2*j+1]) for j in range(reps)])) * 1e-3
 
+
+def varlen(offs, lens, total, seed):
+    n = lens.size
+    buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, seed, None)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev); m = torch.from_numpy(lens.astype(np.int64)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    wsb = lib.nvl_crc32c_batch_workspace_bytes(n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    fn = lambda: lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0,
+                                          ws.data_ptr(), wsb, st)
+    return buf, out, fn, (o, m, ws)
+
+
 for c in a.configs.split(","):
-    c = int(c)
-    if c in (2, 4):
+    keep = None
+    if c in ("2", "4"):
         cfg = g[f"cfg{c}"]; n, L = cfg["n"], cfg["len"]
         buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
         lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, cfg["seed"], None)
@@ -42,24 +65,45 @@ for c in a.configs.split(","):
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         fn = lambda: lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(), wsb, st)
         alg = n * (L + 4)
-    else:
+        check = lambda res: p.digest(res) == cfg["digest"]
+    elif c == "3":
         cfg = g["cfg3"]; total = cfg["total"]
         lens = p.cfg3_lengths(cfg["len_seed"], total)
-        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
         n = lens.size
-        buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
-        lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, cfg["seed"], None)
-        o = torch.from_numpy(offs).to(dev); m = torch.from_numpy(lens.astype(np.int64)).to(dev)
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-        wsb = lib.nvl_crc32c_batch_workspace_bytes(n)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-        fn = lambda: lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0, ws.data_ptr(), wsb, st)
+        buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"])
         alg = total + 12 * n
-    t = timeit(fn, a.reps if c != 4 else max(3, a.reps // 4))
+        check = lambda res: p.digest(res) == cfg["digest"]
+    elif c in ("v", "r"):
+        n = 100_000
+        if c == "v":
+            lens = np.full(n, 4097, dtype=np.int64)
+        else:
+            lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
+        total = int(offs[-1] + lens[-1]) + 4
+        buf, out, fn, keep = varlen(offs, lens, total, 0x5EED00B1)
+        alg = int(lens.sum()) + 20 * n
+        host = buf.cpu().numpy()
+        check = lambda res: bool(np.array_equal(res, p.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64))))
+    elif c == "g":
+        n, L, S, off = 100_000, 4096, 4099, 3
+        buf = torch.empty(off + n * S + 64, dtype=torch.uint8, device=dev)
+        lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), buf.numel() // 8, 8, 0, 1, 0x5EED00B2, None)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        wsb = max(1, lib.nvl_crc32c_fixed_workspace_bytes(S, L, n))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fn = lambda: lib.nvl_crc32c_fixed_dev(buf.data_ptr() + off, S, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(),
+                                              wsb, st)
+        alg = n * (L + 4)
+        host = buf.cpu().numpy()
+        check = lambda res: bool(np.array_equal(res, p.fixed(host[off:], S, L, n)))
+    else:
+        raise SystemExit(f"unknown config {c}")
+    t = timeit(fn, a.reps if c != "4" else max(3, a.reps // 4))
     res = out.cpu().numpy().view(np.uint32)
-    ok = p.digest(res) == cfg["digest"]
     print(json.dumps({"config": c, "n": int(n), "bytes": int(alg), "median_us": round(t * 1e6, 1),
-                      "GB/s": round(alg / t / 1e9, 1), "GiB/s": round((alg) / t / 2**30, 1),
-                      "frac_of_8TBs": round(alg / t / 8e12, 4), "digest_ok": ok}))
-    del buf
+                      "GB/s": round(alg / t / 1e9, 1), "GiB/s": round(alg / t / 2**30, 1),
+                      "frac_of_8TBs": round(alg / t / 8e12, 4), "ok": bool(check(res))}), flush=True)
+    del buf, keep
     torch.cuda.empty_cache()

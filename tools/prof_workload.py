@@ -1,12 +1,20 @@
-"""Fixed workload for rocprofv3 counter passes: config-2 fast path, K launches.
-    python3 tools/prof_workload.py [--lib build/libnvl_crc32c_X.so] [--blocks N] [--launches K]"""
+"""Fixed workloads for rocprofv3 counter passes and kernel traces, K launches each.
+    python3 tools/prof_workload.py [--lib build/libnvl_crc32c_X.so] [--config cfg2|cfg3|var4097]
+                                   [--blocks N] [--launches K]
+cfg2:    N x 4096 B fixed stride (fast path, nvl_crc32c_fixed_dev)
+cfg3:    BASELINE config 3 (1 GiB, 32672 buffers of 512 B..64 KiB packed back to back, nvl_crc32c_batch_dev)
+var4097: N buffers of 4097 B at stride 4101 -- the whole-table verify shape (block | type, then the
+         4-byte stored CRC), through nvl_crc32c_batch_dev
+"""
 import argparse, ctypes, os, sys
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np
 import torch
 from nvlevelz_amd import _lib
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default=None); ap.add_argument("--blocks", type=int, default=100000)
 ap.add_argument("--launches", type=int, default=20); ap.add_argument("--len", type=int, default=4096)
+ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "var4097"])
 a = ap.parse_args()
 lib = _lib.lib
 if a.lib:
@@ -15,13 +23,36 @@ if a.lib:
         f = getattr(lib, name); f.restype = res; f.argtypes = args
 dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
 assert lib.nvl_crc32c_init(0) == 0
-n, L = a.blocks, a.len
-buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
-lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, 0x5EED0001, None)
-out = torch.empty(n, dtype=torch.int32, device=dev)
-ws = torch.empty(max(1, lib.nvl_crc32c_fixed_workspace_bytes(L, L, n)), dtype=torch.uint8, device=dev)
-for _ in range(a.launches):
-    assert lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(),
-                                    ws.numel(), torch.cuda.current_stream().cuda_stream) == 0
+st = torch.cuda.current_stream().cuda_stream
+if a.config == "cfg2":
+    n, L = a.blocks, a.len
+    buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, 0x5EED0001, None)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    ws = torch.empty(max(1, lib.nvl_crc32c_fixed_workspace_bytes(L, L, n)), dtype=torch.uint8, device=dev)
+    for _ in range(a.launches):
+        assert lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(),
+                                        ws.numel(), st) == 0
+else:
+    if a.config == "cfg3":
+        import oracle
+        lens = oracle.port().cfg3_lengths(0x5EED0003, 1 << 30).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        total, seed = 1 << 30, 0x5EED0002
+    else:
+        n = a.blocks
+        lens = np.full(n, 4097, dtype=np.int64)
+        offs = np.arange(n, dtype=np.int64) * 4101
+        total, seed = n * 4101, 0x5EED0001
+    n = lens.size
+    buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, seed, None)
+    o = torch.from_numpy(offs).to(dev)
+    m = torch.from_numpy(lens).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    ws = torch.empty(lib.nvl_crc32c_batch_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    for _ in range(a.launches):
+        assert lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0,
+                                        ws.data_ptr(), ws.numel(), st) == 0
 torch.cuda.synchronize()
-print("done", hex(int(out[0].item()) & 0xFFFFFFFF))
+print("done", a.config, hex(int(out[0].item()) & 0xFFFFFFFF))

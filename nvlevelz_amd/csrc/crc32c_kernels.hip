@@ -46,11 +46,17 @@ constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWave * kWavesPerWG;  // 1024
 constexpr uint32_t kChunk = 4096;
 constexpr uint32_t kUnitsPerWG = 64;  // work units per workgroup (scheduler B)
-// Overhang: a buffer's first chunk may hold up to kOver bytes more than 4096
-// (a 4097..4112-byte buffer is ONE pass -- the n+1-byte CRC of an SSTable
-// data block of 4096..4111 bytes, table/format.cc:90-92); the extra bytes are
-// checksummed as one 16-byte piece beside the chunk's 64 pieces.
-constexpr uint32_t kOver = 16;
+// Overhang (tuning knob, off): a buffer's first chunk may hold up to kOver
+// bytes more than 4096, checksummed as a 16-byte piece beside the chunk's 64
+// pieces (a 4097-byte block|type CRC, table/format.cc:90-92, then is ONE
+// pass).  Off, such a buffer is a 1-byte head (crc32c_head_kernel, P = 1
+// lane) plus one full body chunk, which keeps the body kernels' chunk pass
+// free of the overhang's registers and extra lookups.
+#ifndef NVL_OVER
+#define NVL_OVER 0
+#endif
+constexpr uint32_t kOver = NVL_OVER;
+static_assert(kOver == 0 || kOver == 16, "the overhang piece is 16 bytes");
 
 // Chunks of a buffer of L bytes: END-aligned 4096-byte chunks, the first one
 // 1..4096+kOver bytes long (tests/kernel_model.py chunks_of).
@@ -135,6 +141,11 @@ __device__ __forceinline__ u32x4 ld16(uintptr_t addr) {
   return __builtin_nontemporal_load((gvec_ptr)addr);
 #endif
 }
+
+// The same through the caches: the head kernel's lane-group loads touch each
+// line from several instructions (lanes 64 bytes apart), so non-temporal
+// loads would let a line go before its neighbours read it.
+__device__ __forceinline__ u32x4 ld16c(uintptr_t addr) { return *(gvec_ptr)addr; }
 
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t* lds, uint32_t off) {
   return *reinterpret_cast<const uint32_t*>(lds + off);
@@ -295,10 +306,10 @@ struct KArgs {
   Rec* recs;  // 2 per work unit: [2u] = head portion, [2u+1] = tail portion (or nullptr)
   const uint32_t* tables;
   uint32_t* counter;  // the stream's done counter (fused variable kernel); zero between launches
-  // Head contributions (kGeneral): hc[i] = buffer i's partial first chunk,
-  // normalized to the buffer end, written by crc32c_head_kernel before the
-  // body kernel runs (0 for a buffer without one); nullptr when no buffer of
-  // the batch has a partial first chunk.
+  // Heads (kGeneral): hc[i] = the raw register of buffer i's partial first
+  // chunk when the buffer has more chunks, written by crc32c_head_kernel
+  // before the body kernel runs (only read for such buffers); nullptr when no
+  // buffer of the batch has one.
   uint32_t* hc;
 };
 
@@ -386,11 +397,10 @@ struct VarGeom {
 
 // Load modes: kAligned = 16-B aligned buffer whose length is a multiple of 4096
 // (every chunk full, no masking: configs 2, 4, 5); kGeneral = the full
-// 4096-byte chunks of buffers of any alignment and length (realignment, the
-// overhang); kHead = partial first chunks (they start before the buffer:
-// predicated loads, masking), run by their own kernel so that the body
-// kernel's registers never hold the masking code's (86 vs 128+ VGPRs).
-enum LoadMode : int { kAligned = 0, kGeneral = 1, kHead = 2 };
+// 4096-byte chunks of buffers of any alignment and length (realignment).
+// Partial first chunks (heads) never reach these kernels: crc32c_head_kernel
+// runs them, so the body kernels' registers never hold masking code.
+enum LoadMode : int { kAligned = 0, kGeneral = 1 };
 
 // A buffer's first chunk is a head chunk when it starts before the buffer
 // (partial: 1..4095 bytes) or the buffer is shorter than 4 bytes (bytewise).
@@ -423,11 +433,6 @@ __device__ __forceinline__ uintptr_t chunk_end(const BufInfo& bi, uint32_t c) {
 // Byte offset of the lane's 16 B within each 1 KiB load.
 __device__ __forceinline__ uint32_t lane_load_off(int lane) {
   return ((uint32_t)(lane & 15) << 6) | ((uint32_t)(lane >> 4) << 4);
-}
-
-// A wave-uniform dword through the constant address space (s_load).
-__device__ __forceinline__ uint32_t sload_u32(uintptr_t a) {
-  return *reinterpret_cast<const __attribute__((address_space(4))) uint32_t*>(a);
 }
 
 template <int M>
@@ -464,36 +469,19 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
     const uint32_t r = (uint32_t)(ce & 3u);
     const uintptr_t A4 = ce - kChunk - r;
     const uintptr_t g = (uintptr_t)bi.p & ~(uintptr_t)15;  // granule of the buffer start
-    if constexpr (M == kGeneral) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
-        ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
-      }
-    } else {
-      // kHead: the chunk reaches below p's granule g: a slot wholly below g
-      // is not loaded (zeros); the slot straddling g is loaded from g (its
-      // words are moved into place by build_words -- not here, so that no
-      // instruction waits on this prefetch); the rest load as usual.
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uintptr_t a = A4 + 1024u * (uint32_t)j + lo;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (a + 16u > g) v = ld16(a < g ? g : a);
-        ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
-      }
+    for (int j = 0; j < 4; ++j) {
+      const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
+      ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
     }
     // Edge load: lane 63 when the realign needs the dword past the last
     // piece (r != 0; the 16 bytes end in the chunk's last dword, which holds
-    // byte ce-1), lane 0 when the chunk has an overhang (kGeneral chunk 0
-    // starting after p: the 16 bytes below A4, clamped up to p's granule;
-    // build_words moves them into place).
-    // A head chunk's buffer can be shorter than those 16 bytes: lane 63's
-    // address is then clamped up to g too (edge_dword picks the dword).
-    const bool ovh = M == kGeneral && c == 0 && A4 + r > (uintptr_t)bi.p;
+    // byte ce-1), lane 0 when the chunk has an overhang (chunk 0 starting
+    // after p: the 16 bytes below A4, clamped up to p's granule; build_words
+    // moves them into place).
+    const bool ovh = kOver > 0 && c == 0 && A4 + r > (uintptr_t)bi.p;
     if ((lane == 63 && r != 0) || (lane == 0 && ovh)) {
-      const uintptr_t e63 = M == kHead && A4 + kChunk - 12u < g ? g : A4 + kChunk - 12u;
-      const uintptr_t ea = lane == 63 ? e63 : (A4 - 16u > g ? A4 - 16u : g);
+      const uintptr_t ea = lane == 63 ? A4 + kChunk - 12u : (A4 - 16u > g ? A4 - 16u : g);
       const u32x4 v = ld16(ea);
       ch.e[0] = v.x; ch.e[1] = v.y; ch.e[2] = v.z; ch.e[3] = v.w;
     }
@@ -545,37 +533,12 @@ __device__ __forceinline__ void mask_inject(uint32_t (&w)[NW], int rel, uint32_t
 }
 
 // The lane's 16 words of piece P = lane (64 contiguous bytes), with the ~init
-// injection and, on a head chunk, the zero-masking of bytes before the
-// buffer start.
+// injection.
 template <int M>
 __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int lane, const Chunk& ch,
                                             uint32_t (&w)[16], uint32_t (&ov)[4]) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
-  if constexpr (M == kHead) {
-    // The slot straddling the start granule g was loaded from g: move its
-    // words up by q = (g - a)/4 dwords (q is the same for the whole wave: a
-    // is A4 mod 16); its words below g are before p and masked below.
-    const uintptr_t ce = chunk_end(bi, c);
-    const uintptr_t A4 = ce - kChunk - (ce & 3u);
-    const uintptr_t g = (uintptr_t)bi.p & ~(uintptr_t)15;
-    const uint32_t q = (uint32_t)((g - A4) >> 2) & 3u;
-    if (A4 < g && q != 0) {
-      const uint32_t lo = lane_load_off(lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uintptr_t a = A4 + 1024u * (uint32_t)j + lo;
-        if (a < g && a + 16u > g) {
-          uint32_t* x = w + 4 * j;
-          const uint32_t v0 = x[0], v1 = x[1], v2 = x[2];
-          x[3] = q == 1 ? v2 : (q == 2 ? v1 : v0);
-          x[2] = q == 1 ? v1 : (q == 2 ? v0 : 0u);
-          x[1] = q == 1 ? v0 : 0u;
-          x[0] = 0u;
-        }
-      }
-    }
-  }
 #if !defined(NVL_ABL_NOLOAD)
   row_transpose(w);
 #endif
@@ -589,13 +552,13 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
     // 4-byte aligned address below the chunk start); lane P's bytes continue
     // in lane P+1 and, for lane 63, in its edge dword e[3].
     const uint32_t r = (uint32_t)(ce & 3u);
-    if (M == kGeneral && c == 0 && cs > p) {
+    if (kOver > 0 && c == 0 && cs > p) {
       // Overhang: lane 0 turns the o = cs - p bytes before the chunk into a
       // 16-byte piece ending at cs (bytes before p masked, ~init injected)
       // from its edge load e[] = the 16 bytes below A4 (clamped up to p's
       // granule g: moved up by qq dwords) and its first loaded dword (w[0]
-      // before the realign).  run_units prepends the four words to lane 0's
-      // chain; every other lane prepends zeros, which a zero register ignores.
+      // before the realign).  chain_fold_ov runs the four words as a chain of
+      // their own; every other lane holds zeros (a zero register stays zero).
       const uintptr_t A4 = cs - r;
       const uintptr_t g = p & ~(uintptr_t)15;
       const uint32_t qq = A4 - 16u >= g ? 0u : (uint32_t)(g - (A4 - 16u)) >> 2;
@@ -616,46 +579,21 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
     }
 #if !defined(NVL_ABL_NOREALIGN)
     if (r != 0) {
-      // lane 63's dword past the last piece: e[3], or -- a head chunk whose
-      // edge load was clamped up to p's granule g -- the dword at A4 + 4096
-      uint32_t last = ch.e[3];
-      if constexpr (M == kHead) {
-        const uintptr_t A4 = cs - r;
-        const uintptr_t g = p & ~(uintptr_t)15;
-        if (A4 + kChunk - 12u < g) {
-          const uint32_t x = (uint32_t)(A4 + kChunk - g) >> 2;  // 0..3, wave-uniform
-          last = x == 0 ? ch.e[0] : (x == 1 ? ch.e[1] : (x == 2 ? ch.e[2] : ch.e[3]));
-        }
-      }
-      const uint32_t nx = next_lane(w[0], last);
+      // lane 63's dword past the last piece: its edge load's e[3]
+      const uint32_t nx = next_lane(w[0], ch.e[3]);
 #pragma unroll
       for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
       w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
     }
 #endif
-    if constexpr (M == kHead) {
-#if !defined(NVL_ABL_NOMASK)
-      // bytes before the start masked, ~init injected
-      mask_inject<16>(w, (int)(int64_t)(p - cs) - 64 * (int)opaque((uint32_t)lane), bi.s);
-#endif
-    } else if (c == 0 && cs < p + 4) {
-      // a chunk that starts at the buffer start, or 1..3 bytes after it (the
-      // overhang holds those bytes): ~init, or what the overhang leaves of it,
-      // goes into lane 0's first word
+    if (cs < p + 4) {
+      // a chunk that starts at the buffer start, or 1..3 bytes after it (a
+      // head or the overhang holds those bytes): ~init, or what of it reaches
+      // past them, goes into lane 0's first word (body chunks start at or
+      // after p)
       if (lane == 0) w[0] ^= bi.s >> (8u * (uint32_t)(cs - p));
     }
   }
-}
-
-// lane 0's chain over the overhang piece, folded into its first word: the
-// register the 16-word chain must start from (see build_words).
-__device__ __forceinline__ uint32_t overhang_start(const uint8_t* lds, const LaneBase& lb, const uint32_t (&ov)[4],
-                                                   uint32_t w0) {
-  uint32_t crc = ov[0];
-  crc = slice4_next(lds, crc, ov[1], lb);
-  crc = slice4_next(lds, crc, ov[2], lb);
-  crc = slice4_next(lds, crc, ov[3], lb);
-  return slice4_next(lds, crc, w0, lb);
 }
 
 // Serial slice-by-4 chains + butterflies of U chunks from their built words,
@@ -744,6 +682,32 @@ __device__ __forceinline__ uint32_t chain_fold(const uint8_t* lds, const LaneBas
   return r[0];
 }
 
+// The same for a first chunk with an overhang piece ov (16 bytes before the
+// chunk; nonzero in lane 0 only, see build_words): its raw register runs as a
+// second, independent 4-step chain beside the main one and joins lane 0's
+// chain shifted by that lane's 64-byte piece (comb table 0), so the serial
+// path stays 16 steps + butterfly (as one prepended 20-step chain it was 25 %
+// longer: 4097-byte buffers ran 115 us vs 91 us for 4096-byte ones).
+__device__ __forceinline__ uint32_t chain_fold_ov(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[16],
+                                                  const uint32_t (&ov)[4], int lane) {
+  uint32_t crc = w[0], a = ov[0];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    crc = slice4_next(lds, crc, k < 15 ? w[k + 1] : 0u, lb);
+    if (k < 4) a = slice4_next(lds, a, k < 3 ? ov[k + 1] : 0u, lb);
+  }
+  const uint8_t* c0 = lds + kCombOff;  // comb level 0: shift by 64 bytes, byte j in sub-table j
+  crc ^= xor3(lds_u32(c0, (a & 0xFFu) << 2), lds_u32(c0 + 1024u, ((a >> 8) & 0xFFu) << 2),
+              lds_u32(c0 + 2048u, ((a >> 16) & 0xFFu) << 2)) ^
+         lds_u32(c0 + 3072u, (a >> 24) << 2);
+  crc = fold_level<0, 0, false>(lds, crc, lane);
+  crc = fold_level<1, 1, false>(lds, crc, lane);
+  crc = fold_level<2, 2, false>(lds, crc, lane);
+  crc = fold_level<3, 3, false>(lds, crc, lane);
+  crc = fold_level<4, 4, false>(lds, crc, lane);
+  return fold_level<5, 5, false>(lds, crc, lane);
+}
+
 template <int M>
 __device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo& bi,
                                               uint32_t c, int lane, const Chunk& ch) {
@@ -790,15 +754,16 @@ struct UnitState {
   Rec head;
 };
 
-// hx: the buffer's head contribution when this chunk is its last (kGeneral
-// with a partial first chunk, prefetched from KArgs::hc), else 0.
+// hx: the raw register of the buffer's head (its partial first chunk,
+// prefetched from KArgs::hc) when this chunk is its first body chunk, else 0:
+// the head then enters like a preceding chunk (shift(0) = 0 otherwise).
 __device__ __forceinline__ void consume(UnitState& st, const Pos& p, uint32_t raw, const uint8_t* lds, int lane,
                                         const KArgs& ka, uint32_t hx = 0u) {
-  st.acc = st.cnt ? (shift4096(lds, st.acc, lane) ^ raw) : raw;
+  st.acc = shift4096(lds, st.cnt ? st.acc : hx, lane) ^ raw;
   ++st.cnt;
   if (p.c + 1 == p.bi.J) {
     if (st.from_zero) {
-      if (lane == 0) ka.out[p.i] = finish(~(st.acc ^ hx), ka.flags);
+      if (lane == 0) ka.out[p.i] = finish(~st.acc, ka.flags);
     } else {
       st.head = Rec{p.i, st.acc, st.cnt | kRecEnds};
     }
@@ -976,12 +941,12 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   auto lo_of = [&](uint32_t uu) -> uint64_t { return g.unit_lo(T, uu); };
   // kGeneral: a head chunk (partial first chunk, or a buffer of < 4 bytes)
   // belongs to crc32c_head_kernel: the step that reaches one loads and
-  // computes nothing; the buffer's other chunks add its contribution hc[i]
-  // when they complete it (prefetched with its last chunk, hv).
+  // computes nothing; its raw register hc[i] is prefetched with the buffer's
+  // first body chunk (hv) and shifted in ahead of it.
   auto skip = [&](const Pos& q) -> bool { return M == kGeneral && q.c == 0 && head_first(q.bi.len); };
   auto first_body = [&](const Pos& q) -> uint32_t { return (M == kGeneral && head_first(q.bi.len)) ? 1u : 0u; };
   auto hc_of = [&](const Pos& q) -> uint32_t {  // vector load, in vmcnt order behind the chunk's own loads
-    if (M != kGeneral || !ka.hc || q.c + 1 != q.bi.J || !head_first(q.bi.len)) return 0u;
+    if (M != kGeneral || !ka.hc || q.c != 1u || !head_first(q.bi.len)) return 0u;
     return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)(ka.hc + q.i));
   };
 
@@ -1053,13 +1018,13 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
     if (q1v) load_chunk<M>(q1.bi, q1.c, lane, n1);
     if (work) {
       NVL_COUNT();
-      if (M == kGeneral) {  // a first chunk with an overhang: lane 0's chain starts 16 bytes early
-        if (p0.c == 0 && chunk_end(p0.bi, 0) - kChunk > (uintptr_t)p0.bi.p)
-          w[0][0] = overhang_start(lds, lb, ov[0], w[0][0]);
-      }
+      // a first chunk with an overhang: lane 0's piece starts 16 bytes early
+      const bool ovh = kOver > 0 && M == kGeneral && p0.c == 0 && chunk_end(p0.bi, 0) - kChunk > (uintptr_t)p0.bi.p;
       uint32_t r[2];
       if (two) {
         chains<2, false>(lds, lb, w, lane, r);
+      } else if (ovh) {
+        r[0] = chain_fold_ov(lds, lb, w[0], ov[0], lane);
       } else {
         r[0] = chain_fold<M>(lds, lb, w[0], lane);
       }
@@ -1097,135 +1062,202 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
 
 // ---------------------------------------------------------------------------
 // Head chunks -- crc32c_head_kernel, launched before the kGeneral body
-// kernel of the same batch.  Workgroup b owns buffers [n*b/G, n*(b+1)/G) and
-// takes them kHeadBatch at a time in two phases:
-//   1. classify, lane-parallel (each lane one buffer; waves take groups of
-//      64): a buffer of < 4 bytes is finished bytewise by its lane
-//      (util/crc32c.cc:287 STEP1 semantics), one without a head chunk gets
-//      hc[i] = 0, one with a partial first chunk is appended to an LDS list;
-//   2. the waves pull list items one at a time, each a masked chunk pass, the
-//      next item's chunk loads and the one after's metadata (vector loads, so
-//      nothing in flight couples with the chains' LDS waits) issued before
-//      the current item computes.  A one-chunk buffer is finished (out[i]),
-//      a longer one leaves hc[i] = its head normalized to the buffer end.
-constexpr uint32_t kHeadBatch = 960;                        // list capacity (u32 items)
-constexpr uint32_t kHeadListOff = kLdsBytes;                // after the table image
-constexpr uint32_t kHeadCtrOff = kHeadListOff + 4u * kHeadBatch;  // u32 list_n, queue
-constexpr uint32_t kHeadLdsBytes = kHeadCtrOff + 16u;
-static_assert(kHeadLdsBytes <= 160u * 1024u, "head kernel LDS exceeds 160 KiB");
+// kernel of the same batch.  A head is a buffer's partial first chunk, h =
+// 1..4095 bytes (the whole buffer when it has one chunk).  The chunk pass
+// cuts a chunk into 64-byte pieces, one per lane; a head needs only
+// ceil(h/64) of them, so a wave runs heads in lane groups of P = 1, 4, 16 or
+// 64 lanes (h <= 64, 256, 1024, 4095) -- 64/P heads per round, the chains of
+// a group combined by the first log2(P) butterfly levels.  A round costs the
+// same 16 chain steps whatever P is: a 6-byte log record no longer takes a
+// whole 4 KiB pass.
+// Each wave owns a contiguous range of buffers and takes it 64 at a time
+// (one buffer per lane: its metadata in the lane's registers).  Buffers of
+// < 4 bytes are finished bytewise by their lane (util/crc32c.cc:287 STEP1
+// semantics); the heads of each class go out in rounds, lane group q of a
+// round holding the class's next q-th head (picked from the class's ballot
+// mask and pulled across lanes with ds_bpermute).  The next round's loads are
+// issued before the current round computes.  A one-chunk buffer is finished
+// (out[i]); a longer one leaves hc[i] = its head's raw register, which the
+// body kernel shifts into the buffer's first body chunk.
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t k) {  // k < popcount(m)
+  uint32_t pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = (uint32_t)__builtin_popcountll(m & ((1ull << w) - 1ull));
+    const bool up = k >= c;
+    k -= up ? c : 0u;
+    m = up ? m >> w : m;
+    pos += up ? (uint32_t)w : 0u;
+  }
+  return pos;
+}
 
-struct ItemMeta {  // one item's metadata as vector loads (every lane the same address)
-  uintptr_t p;
-  uint64_t L;
-  uint32_t s;
+struct HeadLane {  // one lane's part of a head round
+  uintptr_t p;     // buffer start
+  uintptr_t ce;    // head end (= start of the first body chunk, or the buffer end)
+  uint32_t s;      // ~init
+  uint32_t src;    // group lane holding the buffer
+  bool ok;         // this lane's group has a head this round
+  bool last;       // the head is the whole buffer (J == 1)
 };
+
+struct HeadData {
+  uint32_t d[20];  // the five 16-byte granules from floor16(piece start)
+};
+
+// The lane's 64-byte piece of its group's head: [ce - 64P + 64k, +64), k =
+// lane mod P.  Only granules holding head bytes are loaded (fault safety:
+// never a granule outside [p, ce)); the rest read as zeros.
+__device__ __forceinline__ void head_load(const HeadLane& h, uint32_t P, int lane, HeadData& hd) {
+  const uintptr_t ps = h.ce - 64u * P + 64u * ((uint32_t)lane & (P - 1u));
+  const uintptr_t g0 = ps & ~(uintptr_t)15;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const uintptr_t G = g0 + 16u * (uint32_t)j;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (h.ok && G + 16u > h.p && G < h.ce) v = ld16c(G);
+    hd.d[4 * j + 0] = v.x; hd.d[4 * j + 1] = v.y; hd.d[4 * j + 2] = v.z; hd.d[4 * j + 3] = v.w;
+  }
+}
+
+// Raw register of the round's heads (every lane of a group holds its head's).
+__device__ __forceinline__ uint32_t head_raw(const uint8_t* lds, const LaneBase& lb, const HeadLane& h,
+                                             const HeadData& hd, uint32_t P, uint32_t nlev, int lane) {
+  const uintptr_t ps = h.ce - 64u * P + 64u * ((uint32_t)lane & (P - 1u));
+  const uint32_t r = (uint32_t)ps & 15u, qd = r >> 2, b = r & 3u;
+  // Dword shift by qd as two masked selects (v_bfi): as ternaries the
+  // compiler turns them into an indexed scratch copy of the array.
+  const uint32_t m2 = opaque(0u - ((qd >> 1) & 1u)), m1 = opaque(0u - (qd & 1u));
+  uint32_t t[18], e[17], w[16];
+#pragma unroll
+  for (int k = 0; k < 18; ++k) t[k] = (hd.d[k + 2] & m2) | (hd.d[k] & ~m2);
+#pragma unroll
+  for (int k = 0; k < 17; ++k) e[k] = (t[k + 1] & m1) | (t[k] & ~m1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(e[k + 1], e[k], b);
+  mask_inject<16>(w, (int)(int64_t)(h.p - ps), h.s);
+  uint32_t crc = w[0];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) crc = slice4_next(lds, crc, k < 15 ? w[k + 1] : 0u, lb);
+  if (nlev > 0) {
+    crc = fold_level<0, 0, false>(lds, crc, lane);
+    crc = fold_level<1, 1, false>(lds, crc, lane);
+  }
+  if (nlev > 2) {
+    crc = fold_level<2, 2, false>(lds, crc, lane);
+    crc = fold_level<3, 3, false>(lds, crc, lane);
+  }
+  if (nlev > 4) {
+    crc = fold_level<4, 4, false>(lds, crc, lane);
+    crc = fold_level<5, 5, false>(lds, crc, lane);
+  }
+  return crc;
+}
 
 template <class G>
 __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t n = g.n;
-  const uint64_t B0 = n * blockIdx.x / gridDim.x, B1 = n * (blockIdx.x + 1) / gridDim.x;
-  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kHeadListOff);
-  uint32_t* list_n = reinterpret_cast<uint32_t*>(lds + kHeadCtrOff);
-  uint32_t* queue = list_n + 1;
-  fill_lds<kWavesPerWG>(lds, ka.tables);
-  const LaneBase lb = make_lane_base(lane);
-  for (uint64_t s0 = B0; s0 < B1; s0 += kHeadBatch) {
-    const uint32_t nb = (uint32_t)min((uint64_t)kHeadBatch, B1 - s0);
-    if (threadIdx.x == 0) {
-      *list_n = 0u;
-      *queue = 0u;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWG;
+  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+  const uint64_t b0 = g.n * gw / nwaves, b1 = g.n * (gw + 1) / nwaves;
+  bool filled = false;
+  LaneBase lb = make_lane_base(lane);
+  for (uint64_t gb = b0;; gb += kWave) {
+    // (every wave reaches the workgroup barrier once, also with an empty range)
+    const bool valid = gb + (uint64_t)lane < b1;
+    const uint64_t i = gb + (uint64_t)lane;
+    uintptr_t lp = 0;
+    uint64_t lL = 0;
+    uint32_t ls = 0;
+    if (valid) g.lane_meta(i, lp, lL, ls);
+    if (!filled) {
+      fill_lds<kWavesPerWG>(lds, ka.tables);
+      __syncthreads();
+      filled = true;
     }
-    __syncthreads();  // (also: the table image is complete)
-    for (uint32_t grp = wv; grp * kWave < nb; grp += kWavesPerWG) {
-      const uint32_t li = grp * kWave + (uint32_t)lane;
-      const uint64_t i = s0 + li;
-      const bool valid = li < nb;
-      uintptr_t lp = 0;
-      uint64_t lL = 0;
-      uint32_t ls = 0;
-      if (valid) g.lane_meta(i, lp, lL, ls);
-      const bool tiny = valid && lL < 4;
-      const bool head = valid && !tiny && head_first(lL);
-      if (tiny) {
-        uint32_t l = ls;  // = ~init
-        for (uint32_t k = 0; k < (uint32_t)lL; ++k) {
-          const uint32_t b = reinterpret_cast<const uint8_t*>(lp)[k];
-          l = lds_u32(lds + kSliceOff, (((l ^ b) & 0xFFu) << 8) | ((uint32_t)(lane & 31) << 2)) ^ (l >> 8);  // T0
-        }
-        ka.out[i] = finish(~l, ka.flags);
-      } else if (valid && !head && ka.hc) {
-        ka.hc[i] = 0u;
+    if (gb >= b1) break;
+    const bool tiny = valid && lL < 4;
+    const uint32_t J = chunks_for(lL);
+    const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);  // first chunk's bytes
+    const bool head = valid && !tiny && hl < kChunk;
+    const uint32_t cls = hl <= 64u ? 0u : (hl <= 256u ? 1u : (hl <= 1024u ? 2u : 3u));
+    if (tiny) {
+      uint32_t l = ls;  // = ~init
+      for (uint32_t k = 0; k < (uint32_t)lL; ++k) {
+        const uint32_t by = reinterpret_cast<const uint8_t*>(lp)[k];
+        l = lds_u32(lds + kSliceOff, (((l ^ by) & 0xFFu) << 8) | ((uint32_t)(lane & 31) << 2)) ^ (l >> 8);  // T0
       }
-      const uint64_t m = __ballot(head);
-      uint32_t base = 0;
-      if (lane == 0 && m)
-        base = __hip_atomic_fetch_add(list_n, (uint32_t)__builtin_popcountll(m), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-      base = __builtin_amdgcn_readfirstlane(base);
-      if (head) list[base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = li;
+      ka.out[i] = finish(~l, ka.flags);
     }
-    __syncthreads();
-    const uint32_t nitems = *list_n;
-    auto pull = [&]() -> uint32_t {
-      uint32_t v = 0;
-      if (lane == 0) v = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return __builtin_amdgcn_readfirstlane(v);
-    };
-    auto meta_load = [&](uint32_t k, ItemMeta& im) {
-      if (k < nitems) g.lane_meta(s0 + list[k], im.p, im.L, im.s);
-    };
-    auto info_of = [&](const ItemMeta& im) -> BufInfo {
-      const uint64_t L = uniform_u64(im.L);
-      return BufInfo{reinterpret_cast<const uint8_t*>(uniform_u64(im.p)), L, chunks_for(L), uniform_u32(im.s)};
-    };
-    uint32_t k = pull();
-    if (k < nitems) {
-      ItemMeta mc{}, mn{};
-      meta_load(k, mc);
-      BufInfo bi = info_of(mc);
-      Chunk cur;
-      load_chunk<kHead>(bi, 0, lane, cur);
-      uint32_t kn = pull();
-      meta_load(kn, mn);
-      while (true) {
-        uint32_t w[16], ov[4];
-        build_words<kHead>(bi, 0, lane, cur, w, ov);
-        const bool more = kn < nitems;
-        BufInfo bn = bi;
-        Chunk nxt;
-        uint32_t knn = nitems;
-        ItemMeta mnn{};
-        if (more) {
-          bn = info_of(mn);
-          load_chunk<kHead>(bn, 0, lane, nxt);
-          knn = pull();
-          meta_load(knn, mnn);
-        }
-        const uint32_t raw = chain_fold<kHead>(lds, lb, w, lane);
-        const uint64_t ib = s0 + list[k];
-        if (bi.J == 1) {
-          if (lane == 0) ka.out[ib] = finish(~raw, ka.flags);
-        } else {
-          const uint32_t nv = normalize(lds, ka.tables, raw, bi.J - 1u, lane);
-          if (lane == 0) ka.hc[ib] = nv;
-        }
-        if (!more) break;
-        k = kn;
-        kn = knn;
-        bi = bn;
-        mn = mnn;
-        cur = nxt;
+    uint64_t m[4];
+    uint32_t nr[4], NR = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      m[c] = __ballot(head && cls == (uint32_t)c);
+      const uint32_t per = 64u >> (2 * c);
+      nr[c] = ((uint32_t)__builtin_popcountll(m[c]) + per - 1u) / per;
+      NR += nr[c];
+    }
+    // Round R -> class c and the class's round t (wave-uniform), then each
+    // lane's head: lane group q = lane / P takes the class's (t*64/P + q)-th.
+    auto setup = [&](uint32_t R, HeadLane& h, uint32_t& P, uint32_t& nlev) {
+      uint32_t c = 0, t = R;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const bool past = c == (uint32_t)k && t >= nr[k];
+        t -= past ? nr[k] : 0u;
+        c += past ? 1u : 0u;
       }
+      nlev = 2u * c;
+      P = 1u << nlev;
+      const uint64_t mc = c == 0 ? m[0] : (c == 1 ? m[1] : (c == 2 ? m[2] : m[3]));
+      const uint32_t per = 64u >> nlev;
+      const uint32_t rank = t * per + ((uint32_t)lane >> nlev);
+      h.ok = rank < (uint32_t)__builtin_popcountll(mc);
+      const uint32_t src = h.ok ? nth_set_bit(mc, rank) : (uint32_t)lane;
+      const int sa = (int)(src << 2);
+      const uint32_t plo = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)lp);
+      const uint32_t phi = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)(lp >> 32));
+      const uint32_t hh = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)hl);
+      h.s = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)ls);
+      const uint32_t jj = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)J);
+      h.p = ((uintptr_t)phi << 32) | plo;
+      h.ce = h.p + hh;
+      h.src = src;
+      h.last = jj == 1u;
+    };
+    if (NR == 0) continue;
+    HeadLane hc0;
+    HeadData dc;
+    uint32_t P0, L0;
+    setup(0, hc0, P0, L0);
+    head_load(hc0, P0, lane, dc);
+    for (uint32_t R = 0; R < NR; ++R) {
+      HeadLane hn = hc0;
+      HeadData dn;
+      uint32_t P1 = P0, L1 = L0;
+      if (R + 1 < NR) {
+        setup(R + 1, hn, P1, L1);
+        head_load(hn, P1, lane, dn);
+      }
+      const uint32_t raw = head_raw(lds, lb, hc0, dc, P0, L0, lane);
+      if (hc0.ok && ((uint32_t)lane & (P0 - 1u)) == 0u) {
+        const uint64_t ib = gb + hc0.src;
+        if (hc0.last) ka.out[ib] = finish(~raw, ka.flags);
+        else ka.hc[ib] = raw;
+      }
+      hc0 = hn;
+      dc = dn;
+      P0 = P1;
+      L0 = L1;
     }
-    __syncthreads();  // the list is reused by the next batch
   }
 }
 
 template <class G>
 __global__ __launch_bounds__(kThreads, 1) void crc32c_head_kernel(G g, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   run_heads(g, ka, lds);
 }
 
@@ -1381,8 +1413,7 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t
 // step (one record pair per lane), so a buffer spanning thousands of units
 // costs tens of steps, not thousands of serial ones.
 __global__ __launch_bounds__(256) void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
-                                                           uint32_t* __restrict__ out, uint32_t flags,
-                                                           const uint32_t* __restrict__ hc) {
+                                                           uint32_t* __restrict__ out, uint32_t flags) {
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (w >= nw) return;
@@ -1406,7 +1437,7 @@ __global__ __launch_bounds__(256) void crc32c_fixup_kernel(const Rec* __restrict
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
-  if (lane == 0) out[h.buf] = finish(~(acc ^ (hc ? hc[h.buf] : 0u)), flags);
+  if (lane == 0) out[h.buf] = finish(~acc, flags);
 }
 
 // ---------------------------------------------------------------------------
@@ -1632,7 +1663,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     const Rec h = lr[2 * t];
     if (h.buf != kNoBuf && (h.cnt & kRecEnds)) {
       uint32_t total = h.raw;
-      if (fold_back(lr, (int)t, h.buf, total)) ka.out[h.buf] = finish(~(total ^ (ka.hc ? ka.hc[h.buf] : 0u)), ka.flags);
+      if (fold_back(lr, (int)t, h.buf, total)) ka.out[h.buf] = finish(~total, ka.flags);
       else edge[0] = Rec{h.buf, total, kRecEnds};  // began before C0
     }
   } else if (t == kUnitsPerWG) {  // the buffer of the range's last chunk, if it runs past C1
@@ -1685,7 +1716,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
       }
       if (ei.buf != kNoBuf || eo.buf != kNoBuf) break;  // unreachable for a consistent plan
     }
-    ka.out[e.buf] = finish(~(total ^ (ka.hc ? ka.hc[e.buf] : 0u)), ka.flags);
+    ka.out[e.buf] = finish(~total, ka.flags);
   }
   if (t == 0) (void)__hip_atomic_exchange((gu32*)ka.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   NVL_FSTAMP(7);
@@ -1721,15 +1752,14 @@ hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64
   return hipGetLastError();
 }
 
-static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, uint32_t* out, uint32_t flags, const uint32_t* hc,
-                                      hipStream_t st, hipEvent_t ev_stop = nullptr) {
+static inline hipError_t launch_fixup(const Rec* recs, uint32_t nw, uint32_t* out, uint32_t flags, hipStream_t st,
+                                      hipEvent_t ev_stop = nullptr) {
   const uint32_t wpb = 4;  // one wave per unit
   const dim3 grid((nw + wpb - 1) / wpb), block(dev::kWave * wpb);
   if (ev_stop)
-    hipExtLaunchKernelGGL(dev::crc32c_fixup_kernel, grid, block, 0, st, nullptr, ev_stop, 0u, recs, nw, out, flags,
-                          hc);
+    hipExtLaunchKernelGGL(dev::crc32c_fixup_kernel, grid, block, 0, st, nullptr, ev_stop, 0u, recs, nw, out, flags);
   else
-    hipLaunchKernelGGL(dev::crc32c_fixup_kernel, grid, block, 0, st, recs, nw, out, flags, hc);
+    hipLaunchKernelGGL(dev::crc32c_fixup_kernel, grid, block, 0, st, recs, nw, out, flags);
   return hipGetLastError();
 }
 
@@ -1746,8 +1776,9 @@ static inline uint32_t chunks_of(uint64_t len) { return dev::chunks_for(len); }
 template <class G>
 static hipError_t launch_heads(const LaunchCtx& lc, const G& g, uint32_t* out, uint32_t flags, uint32_t* hc,
                                hipEvent_t ev_start) {
-  const uint64_t groups = (g.n + dev::kWave - 1) / dev::kWave;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)lc.num_cu, groups));
+  const uint64_t per_wg = 8u * dev::kWavesPerWG;  // at least ~8 buffers per wave
+  const uint32_t grid =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)lc.num_cu, (g.n + per_wg - 1) / per_wg));
   const dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, hc};
   if (ev_start)
     hipExtLaunchKernelGGL(dev::crc32c_head_kernel<G>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, ev_start,
@@ -1813,7 +1844,7 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || J == 1) return e;
-  return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, hc, lc.stream, lc.ev_stop);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, lc.stream, lc.ev_stop);
 }
 
 size_t var_recs_bytes(int num_cu) { return 2ull * (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(Rec); }
@@ -1883,7 +1914,7 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
   hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0, lc.stream, g, ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, hc, lc.stream);
+  return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, lc.stream);
 }
 
 }  // namespace nvl

@@ -99,12 +99,13 @@ def wave_fold(g):
     return g[0]
 
 
-OVER = 16  # overhang: a first chunk of up to 4096 + OVER bytes is ONE pass
+OVER = 0  # overhang (NVL_OVER, off): a first chunk of up to 4096 + OVER bytes is ONE pass
 
 
 def chunks_of(L: int) -> int:
     """Chunks of a buffer of L bytes (crc32c_kernels.hip chunks_for): END-aligned
-    4096-byte chunks; a first chunk of 4097..4096+OVER bytes is not split."""
+    4096-byte chunks (with an overhang, a first chunk of 4097..4096+OVER bytes
+    is not split)."""
     return 1 if L <= CHUNK + OVER else (L - OVER + CHUNK - 1) // CHUNK
 
 
@@ -125,16 +126,68 @@ def _mask_inject(words, rel: int, s: int):
     return out
 
 
+def group_fold(g, nlev: int):
+    """The first nlev butterfly levels over a lane group (fold_level<0..nlev-1>)."""
+    g = list(g)
+    for lev in range(nlev):
+        new = []
+        for l in range(len(g)):
+            pt = g[l ^ (1 << lev)]
+            hi = (l >> lev) & 1
+            left, right = (pt, g[l]) if hi else (g[l], pt)
+            new.append(apply_op(COMB[lev], left) ^ right)
+        g = new
+    assert len(set(g)) == 1
+    return g[0]
+
+
+def head_class(hl: int) -> int:
+    """Lanes per head (crc32c_kernels.hip run_heads): 64-byte pieces, P = 1, 4, 16, 64."""
+    return 1 if hl <= 64 else 4 if hl <= 256 else 16 if hl <= 1024 else 64
+
+
+def head_raw(mem: bytes, p: int, L: int, J: int, s: int) -> int:
+    """Raw register of buffer [p, p+L)'s head (partial first chunk, 1..4095
+    bytes) the way head_load / head_raw run it: a group of P lanes, lane k's
+    piece [ce - 64P + 64k, +64) from the five 16-byte granules at its floor16,
+    granules outside [p, ce) not loaded."""
+    hl = L - CHUNK * (J - 1)
+    assert 4 <= hl < CHUNK or (J > 1 and 1 + OVER <= hl < CHUNK)
+    ce = p + hl
+    P = head_class(hl)
+    lanes = []
+    for k in range(P):
+        ps = ce - 64 * P + 64 * k
+        g0 = ps & ~15
+        d = bytearray(80)
+        for j in range(5):
+            G = g0 + 16 * j
+            if G + 16 > p and G < ce:
+                # fault safety: only granules holding bytes of [p, ce)
+                assert (p & ~15) <= G <= ((ce - 1) & ~15), (G, p, ce)
+                d[16 * j:16 * j + 16] = mem[G:G + 16]
+        r = ps & 15
+        words = [int.from_bytes(d[r + 4 * q:r + 4 * q + 4], "little") for q in range(16)]
+        words = _mask_inject(words, p - ps, s)
+        crc = 0
+        for w in words:
+            crc = slice4(crc ^ w)
+        lanes.append(crc)
+    return group_fold(lanes, P.bit_length() - 1)
+
+
 def chunk_raw(mem: bytes, p: int, L: int, J: int, c: int, s: int) -> int:
     """Raw register of chunk c of buffer [p, p+L) with ~init = s injected,
-    computed the way load_chunk<kGeneral> / build_words<kGeneral> do it."""
+    computed the way load_chunk<kGeneral> / build_words<kGeneral> do it (a
+    partial first chunk: the head kernel's lane groups, head_raw)."""
     e = p + L
+    if c == 0 and e - CHUNK * (J - 1) - CHUNK < p:
+        return head_raw(mem, p, L, J, s)
     ce = e - CHUNK * (J - 1 - c)
     cs = ce - CHUNK
     r = ce & 3
     A4 = cs - r  # every chunk is loaded from the 4-byte aligned address below its start
     g = p & ~15
-    head = cs < p
 
     def load(a: int, n: int) -> bytes:
         # fault safety: only 16-B granules that hold buffer bytes are touched
@@ -143,26 +196,16 @@ def chunk_raw(mem: bytes, p: int, L: int, J: int, c: int, s: int) -> int:
 
     slots = bytearray(CHUNK + 4)
     for k in range(CHUNK // 16):
-        a = A4 + 16 * k
-        if head and a + 16 <= g:
-            continue  # wholly before the granule of p: not loaded (zeros)
-        if head and a < g:
-            d = load(g, 16)  # clamped to p's granule, then moved up by g - a bytes
-            slots[16 * k + (g - a):16 * k + 16] = d[:16 - (g - a)]
-        else:
-            slots[16 * k:16 * k + 16] = load(a, 16)
-    if r:  # lane 63's 16-byte edge load ending at A4 + 4100, clamped up to g (a short head's buffer)
-        ea = max(A4 + CHUNK - 12, g)
-        edge = load(ea, 16)
-        slots[CHUNK:CHUNK + 4] = edge[A4 + CHUNK - ea:A4 + CHUNK - ea + 4]
+        slots[16 * k:16 * k + 16] = load(A4 + 16 * k, 16)
+    if r:  # lane 63's 16-byte edge load ending at A4 + 4100
+        edge = load(A4 + CHUNK - 12, 16)
+        slots[CHUNK:CHUNK + 4] = edge[12:16]
     lanes = []
     for lane in range(64):
         piece = slots[r + 64 * lane:r + 64 * lane + 64]  # bytes [cs + 64 lane, +64)
         words = [int.from_bytes(piece[4 * k:4 * k + 4], "little") for k in range(16)]
-        if head:
-            words = _mask_inject(words, p - (cs + 64 * lane), s)
-        elif c == 0 and lane == 0 and p <= cs < p + 4:
-            words[0] ^= s >> (8 * (cs - p))  # ~init, or what the overhang leaves of it
+        if lane == 0 and p <= cs < p + 4:
+            words[0] ^= s >> (8 * (cs - p))  # ~init, or what a 1..3-byte head / the overhang leaves of it
         crc = 0
         for w in words:
             crc = slice4(crc ^ w)

@@ -100,8 +100,8 @@ def test_general_path_model(port, seed):
     mem = bytes(port.fill(1000 + seed, 0, 120000))
     bufs, pos = [], 64
     for _ in range(rng.randrange(1, 7)):
-        L = rng.choice([0, 1, 2, 3, 4, 5, 17, 63, 64, 65, 4095, 4096, 4097, 4100, 4109, 4112, 4113, 8192, 8208,
-                        8209, 9000, 13000, 20000])
+        L = rng.choice([0, 1, 2, 3, 4, 5, 17, 63, 64, 65, 255, 256, 257, 1000, 1024, 1025, 3000, 4095, 4096, 4097,
+                        4100, 4109, 4112, 4113, 4156, 4196, 4396, 6096, 8191, 8192, 8208, 8209, 9000, 13000, 20000])
         pos += rng.randrange(0, 40)
         bufs.append((pos, L))
         pos += L
@@ -112,14 +112,17 @@ def test_general_path_model(port, seed):
     assert got == want
 
 
-def test_overhang_alignment_sweep_model(port):
+@pytest.mark.parametrize("over", [0, 16])
+def test_overhang_alignment_sweep_model(port, over, monkeypatch):
     """Every start alignment mod 16 x lengths around the chunk and overhang
     boundaries (4096, 4096 + OVER) through the model, with garbage before and
     after each buffer; the model also asserts that no load touches a 16-byte
     granule without buffer bytes (fault safety)."""
-    mem = bytes(port.fill(0xA11, 0, 140000))
-    lens = [4, 5, 6, 7, 15, 16, 17, 63, 64, 65, 4095, 4096, 4097, 4098, 4099, 4100, 4101, 4108, 4111, 4112,
-            4113, 4114, 8207, 8208, 8209, 8210, 8212]
+    monkeypatch.setattr(km, "OVER", over)  # the shipped kernels: NVL_OVER = 0 (a tuning build: 16)
+    mem = bytes(port.fill(0xA11, 0, 200000))
+    lens = [4, 5, 6, 7, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1023, 1024, 1025, 4095, 4096, 4097, 4098, 4099,
+            4100, 4101, 4108, 4111, 4112, 4113, 4114, 4160, 4161, 4352, 4353, 5120, 5121, 8191, 8207, 8208, 8209,
+            8210, 8212]
     for a in range(16):
         bufs = []
         pos = 4096 + a

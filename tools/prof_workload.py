@@ -5,6 +5,8 @@ cfg2:    N x 4096 B fixed stride (fast path, nvl_crc32c_fixed_dev)
 cfg3:    BASELINE config 3 (1 GiB, 32672 buffers of 512 B..64 KiB packed back to back, nvl_crc32c_batch_dev)
 var4097: N buffers of 4097 B at stride 4101 -- the whole-table verify shape (block | type, then the
          4-byte stored CRC), through nvl_crc32c_batch_dev
+gen:     N x 4096 B at stride 4099 from an odd base (fixed-stride general path)
+rand:    N buffers of 3364..4109 B at stride length+4 (data blocks at block_size 4096), batch_dev
 """
 import argparse, ctypes, os, sys
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -14,7 +16,7 @@ from nvlevelz_amd import _lib
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default=None); ap.add_argument("--blocks", type=int, default=100000)
 ap.add_argument("--launches", type=int, default=20); ap.add_argument("--len", type=int, default=4096)
-ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "var4097"])
+ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "var4097", "gen", "rand"])
 a = ap.parse_args()
 lib = _lib.lib
 if a.lib:
@@ -24,14 +26,15 @@ if a.lib:
 dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
 assert lib.nvl_crc32c_init(0) == 0
 st = torch.cuda.current_stream().cuda_stream
-if a.config == "cfg2":
+if a.config in ("cfg2", "gen"):
     n, L = a.blocks, a.len
-    buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
-    lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, 0x5EED0001, None)
+    S, off = (L, 0) if a.config == "cfg2" else (L + 3, 3)
+    buf = torch.empty(off + n * S + 64, dtype=torch.uint8, device=dev)
+    lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), buf.numel() // 8, 8, 0, 1, 0x5EED0001, None)
     out = torch.empty(n, dtype=torch.int32, device=dev)
-    ws = torch.empty(max(1, lib.nvl_crc32c_fixed_workspace_bytes(L, L, n)), dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(1, lib.nvl_crc32c_fixed_workspace_bytes(S, L, n)), dtype=torch.uint8, device=dev)
     for _ in range(a.launches):
-        assert lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(),
+        assert lib.nvl_crc32c_fixed_dev(buf.data_ptr() + off, S, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(),
                                         ws.numel(), st) == 0
 else:
     if a.config == "cfg3":
@@ -41,9 +44,12 @@ else:
         total, seed = 1 << 30, 0x5EED0002
     else:
         n = a.blocks
-        lens = np.full(n, 4097, dtype=np.int64)
-        offs = np.arange(n, dtype=np.int64) * 4101
-        total, seed = n * 4101, 0x5EED0001
+        if a.config == "var4097":
+            lens = np.full(n, 4097, dtype=np.int64)
+        else:
+            lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]]).astype(np.int64)
+        total, seed = int(offs[-1] + lens[-1]) + 4, 0x5EED0001
     n = lens.size
     buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
     lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, seed, None)

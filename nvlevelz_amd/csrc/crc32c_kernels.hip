@@ -1061,6 +1061,165 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
 }
 
 // ---------------------------------------------------------------------------
+// Scheduler B, pipelined (kGeneral; NVL_GEN_PP): the same work units and
+// records as run_units, with two chunk buffers A and B in ping-pong.  A
+// generator walks the chunk stream (pulling units from the LDS counter as it
+// goes); each buffer is refilled from it right after its words are built, so
+// a chunk's loads have two chunk passes to arrive instead of one (with one in
+// flight per wave the waves waited on memory ~half their cycles: general
+// chunks ran at 4.6 TB/s, aligned pairs at 6.3).  Every refill issues the
+// same loads whatever the chunk (a head chunk, or past the end of the work:
+// reads of the table blob, unused), so the compiler's wait counts at the loop
+// head keep the other buffer in flight.
+struct ChunkP {
+  uint32_t d[16];
+  uint32_t e;   // the dword at A4 + 4096 (lane 63's realign word)
+  uint32_t hv;  // hc[i] when this is the buffer's first body chunk (see hv_used)
+};
+
+struct Slot {  // wave-uniform: what a buffer holds
+  Pos pos;
+  uint32_t u;
+  bool valid, start, end, work;
+};
+
+__device__ __forceinline__ void load_chunk_pp(const Slot& s, int lane, uintptr_t safe, const uint32_t* hc,
+                                              ChunkP& ch) {
+  const uintptr_t ce = chunk_end(s.pos.bi, s.pos.c);
+  const uint32_t r = (uint32_t)(ce & 3u);
+  const uintptr_t A4 = s.work ? ce - kChunk - r : safe;
+  const uint32_t lo = lane_load_off(lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
+    ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+  }
+  // r != 0: the dword past the chunk's last piece (holds byte ce-1); r == 0:
+  // the chunk's last dword (unused) -- every lane loads it, one line
+  ch.e = *(const __attribute__((address_space(1))) uint32_t*)(A4 + (r ? kChunk : kChunk - 4u));
+  const uintptr_t ha = hc && s.work ? (uintptr_t)(hc + s.pos.i) : safe;
+  ch.hv = __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)ha);
+}
+
+template <int NW, class G>
+__device__ __forceinline__ void run_units_pp(const G& g, const KArgs& ka, uint8_t* lds) {
+  static_assert(kOver == 0, "the pipelined loop has no overhang piece");
+  NVL_STAMP0();
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t T = g.total();
+  const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
+  const uintptr_t safe = (uintptr_t)ka.tables;  // >= 4100 valid bytes
+  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.unit_lo(T, uu); };
+  auto first_body = [&](const Pos& q) -> uint32_t { return head_first(q.bi.len) ? 1u : 0u; };
+  const Rec none{kNoBuf, 0u, 0u};
+
+  // generator: the unit being walked, its next chunk, its end
+  uint32_t gu = ub0 + wv;
+  uint64_t gt = lo_of(gu), gt1 = lo_of(gu + 1);
+  bool fresh = true, done = false, synced = false;
+  Pos last{};
+  auto gen = [&](Slot& sl) {
+    sl.valid = false;
+    sl.work = false;
+    while (!done && gt >= gt1) {  // unit exhausted (or empty): the next one
+      if (!synced) return;        // (no pulls before the workgroup barrier)
+      gu = ub0 + pull_unit(lds, lane);
+      if (gu >= ub1) {
+        done = true;
+        return;
+      }
+      gt = lo_of(gu);
+      gt1 = lo_of(gu + 1);
+      fresh = true;
+      if (gt >= gt1 && lane == 0) g.put_recs(ka, lds, gu, none, none);  // an empty unit
+    }
+    if (done) return;
+    sl.valid = true;
+    sl.u = gu;
+    sl.start = fresh;
+    sl.end = gt + 1 == gt1;
+    sl.pos = fresh ? unit_start_pos(g, gu, gt) : next_pos(g, last);
+    sl.work = !(sl.pos.c == 0 && head_first(sl.pos.bi.len));
+    last = sl.pos;
+    fresh = sl.end;
+    ++gt;
+  };
+  auto hv_used = [&](const Slot& sl) -> bool { return ka.hc && sl.pos.c == 1u && head_first(sl.pos.bi.len); };
+
+  Slot sA, sB;
+  ChunkP cA, cB;
+  if (gt >= gt1 && lane == 0) g.put_recs(ka, lds, gu, none, none);  // the pre-assigned unit is empty
+  gen(sA);  // the first two chunks of the pre-assigned unit load during the LDS fill
+  load_chunk_pp(sA, lane, safe, ka.hc, cA);
+  asm volatile("" ::: "memory");
+  gen(sB);
+  load_chunk_pp(sB, lane, safe, ka.hc, cB);
+  fill_lds<NW>(lds, ka.tables);
+  __syncthreads();
+  synced = true;
+  const LaneBase lb = make_lane_base(lane);
+  NVL_STAMP1();
+
+  UnitState st{0u, 0u, true, none};
+  Rec tail = none;
+  // One buffer: build its words (the buffer dies), refill it from the
+  // generator, then run the chains and the unit bookkeeping.
+  auto step = [&](Slot& sl, ChunkP& ch) {
+    if (!sl.valid) {  // (only B right after the barrier: its unit had one chunk)
+      gen(sl);
+      load_chunk_pp(sl, lane, safe, ka.hc, ch);
+      return;
+    }
+    if (sl.start) {
+      st = UnitState{0u, 0u, sl.pos.c <= first_body(sl.pos), none};
+      tail = none;
+    }
+    const Slot cur = sl;
+    uint32_t w[16], ov[4];
+    const uint32_t hx = hv_used(cur) ? ch.hv : 0u;
+    if (cur.work) {
+      Chunk c1;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) c1.d[k] = ch.d[k];
+      c1.e[3] = ch.e;
+      build_words<kGeneral>(cur.pos.bi, cur.pos.c, lane, c1, w, ov);
+    }
+    gen(sl);
+    load_chunk_pp(sl, lane, safe, ka.hc, ch);
+    asm volatile("" ::: "memory");
+    if (cur.work) {
+      NVL_COUNT();
+      const uint32_t r = chain_fold<kGeneral>(lds, lb, w, lane);
+      consume(st, cur.pos, r, lds, lane, ka, hx);
+    }
+    if (cur.end) {
+      if (st.cnt) {  // the unit ends inside a buffer: its portion, normalized to the buffer end
+        const uint32_t norm = normalize(lds, ka.tables, st.acc, cur.pos.bi.J - 1u - cur.pos.c, lane);
+        if (st.from_zero) tail = Rec{cur.pos.i, norm, st.cnt};
+        else st.head = Rec{cur.pos.i, norm, st.cnt};
+      }
+      if (lane == 0) g.put_recs(ka, lds, cur.u, st.head, tail);
+    }
+  };
+  while (true) {  // (an invalid slot past the end loads the table blob and does nothing)
+    step(sA, cA);
+    step(sB, cB);
+    if (done && !sA.valid && !sB.valid) break;
+  }
+  NVL_STAMP_END();
+}
+
+#ifndef NVL_GEN_PP
+#define NVL_GEN_PP 0  // kGeneral chunks: 1 = run_units_pp (two chunks in flight per wave; measured no faster, more SGPR spills), 0 = run_units
+#endif
+template <int NW, class G>
+__device__ __forceinline__ void run_general(const G& g, const KArgs& ka, uint8_t* lds) {
+  if constexpr (NVL_GEN_PP) run_units_pp<NW>(g, ka, lds);
+  else run_units<kGeneral, NW>(g, ka, lds);
+}
+
+// ---------------------------------------------------------------------------
 // Head chunks -- crc32c_head_kernel, launched before the kGeneral body
 // kernel of the same batch.  A head is a buffer's partial first chunk, h =
 // 1..4095 bytes (the whole buffer when it has one chunk).  The chunk pass
@@ -1092,50 +1251,89 @@ __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t k) {  // k 
   return pos;
 }
 
-struct HeadLane {  // one lane's part of a head round
+struct HeadLane {  // one lane's part of a head round (5 VGPRs: three rounds are live)
   uintptr_t p;     // buffer start
-  uintptr_t ce;    // head end (= start of the first body chunk, or the buffer end)
+  uint32_t hl;     // head bytes: the head is [p, p + hl)
   uint32_t s;      // ~init
-  uint32_t src;    // group lane holding the buffer
-  bool ok;         // this lane's group has a head this round
-  bool last;       // the head is the whole buffer (J == 1)
+  uint32_t tag;    // group lane holding the buffer | kHeadOk | kHeadLast
 };
+constexpr uint32_t kHeadOk = 1u << 8;    // this lane's group has a head this round
+constexpr uint32_t kHeadLast = 1u << 9;  // the head is the whole buffer (J == 1)
 
 struct HeadData {
-  uint32_t d[20];  // the five 16-byte granules from floor16(piece start)
+  uint32_t d[17];  // 64 bytes from the 4-byte aligned address at or below the piece start, + 1 dword
 };
 
-// The lane's 64-byte piece of its group's head: [ce - 64P + 64k, +64), k =
-// lane mod P.  Only granules holding head bytes are loaded (fault safety:
-// never a granule outside [p, ce)); the rest read as zeros.
-__device__ __forceinline__ void head_load(const HeadLane& h, uint32_t P, int lane, HeadData& hd) {
-  const uintptr_t ps = h.ce - 64u * P + 64u * ((uint32_t)lane & (P - 1u));
-  const uintptr_t g0 = ps & ~(uintptr_t)15;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const uintptr_t G = g0 + 16u * (uint32_t)j;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (h.ok && G + 16u > h.p && G < h.ce) v = ld16c(G);
-    hd.d[4 * j + 0] = v.x; hd.d[4 * j + 1] = v.y; hd.d[4 * j + 2] = v.z; hd.d[4 * j + 3] = v.w;
-  }
+// The lane's 64-byte piece of its group's head: [ce - 64P + 64k, +64), ce =
+// p + hl, k = lane mod P, loaded as four 16-byte slots from A4 (the 4-byte
+// aligned address at or below it) plus the dword at A4 + 64.  Fault safety:
+// a slot wholly below p's 16-byte granule g is not loaded (zeros); the slot
+// straddling g is loaded from g (head_words moves its words up); nothing
+// reaches past the head's last dword.
+__device__ __forceinline__ uintptr_t head_piece(const HeadLane& h, uint32_t P, int lane) {
+  return h.p + h.hl - 64u * P + 64u * ((uint32_t)lane & (P - 1u));
 }
 
-// Raw register of the round's heads (every lane of a group holds its head's).
-__device__ __forceinline__ uint32_t head_raw(const uint8_t* lds, const LaneBase& lb, const HeadLane& h,
-                                             const HeadData& hd, uint32_t P, uint32_t nlev, int lane) {
-  const uintptr_t ps = h.ce - 64u * P + 64u * ((uint32_t)lane & (P - 1u));
-  const uint32_t r = (uint32_t)ps & 15u, qd = r >> 2, b = r & 3u;
-  // Dword shift by qd as two masked selects (v_bfi): as ternaries the
-  // compiler turns them into an indexed scratch copy of the array.
-  const uint32_t m2 = opaque(0u - ((qd >> 1) & 1u)), m1 = opaque(0u - (qd & 1u));
-  uint32_t t[18], e[17], w[16];
+// Every load is issued unconditionally (a slot that holds no head bytes reads
+// `safe` -- p's own granule, or any valid address when the lane's group has
+// no head -- and is zeroed in head_words): loads behind branches would make
+// the compiler wait for every load in flight (vmcnt(0)) before each round.
+__device__ __forceinline__ bool head_slot_used(const HeadLane& h, uintptr_t A4, uintptr_t g, int j) {
+  return (h.tag & kHeadOk) != 0u && A4 + 16u * (uint32_t)j + 16u > g;
+}
+__device__ __forceinline__ bool head_edge_used(const HeadLane& h, uintptr_t ps, uintptr_t g) {
+  return (h.tag & kHeadOk) != 0u && (ps & 3u) != 0u && (ps & ~(uintptr_t)3) + 68u > g;
+}
+
+__device__ __forceinline__ void head_load(const HeadLane& h, uint32_t P, int lane, uintptr_t safe, HeadData& hd) {
+  const uintptr_t ps = head_piece(h, P, lane);
+  const uintptr_t A4 = ps & ~(uintptr_t)3;
+  const uintptr_t g = h.p & ~(uintptr_t)15;
+  const uintptr_t sf = (h.tag & kHeadOk) ? g : safe;
 #pragma unroll
-  for (int k = 0; k < 18; ++k) t[k] = (hd.d[k + 2] & m2) | (hd.d[k] & ~m2);
+  for (int j = 0; j < 4; ++j) {
+    const uintptr_t a = A4 + 16u * (uint32_t)j;
+    const u32x4 v = ld16c(head_slot_used(h, A4, g, j) ? (a < g ? g : a) : sf);
+    hd.d[4 * j + 0] = v.x; hd.d[4 * j + 1] = v.y; hd.d[4 * j + 2] = v.z; hd.d[4 * j + 3] = v.w;
+  }
+  hd.d[16] = *(const __attribute__((address_space(1))) uint32_t*)(head_edge_used(h, ps, g) ? A4 + 64u : sf);
+}
+
+// The lane's 16 words of its piece: unused slots zeroed, the slot straddling
+// g moved into place, realigned to the piece start, bytes before p masked,
+// ~init injected.
+__device__ __forceinline__ void head_words(const HeadLane& h, const HeadData& hd, uint32_t P, int lane,
+                                           uint32_t (&w)[16]) {
+  const uintptr_t ps = head_piece(h, P, lane);
+  const uintptr_t A4 = ps & ~(uintptr_t)3;
+  const uintptr_t g = h.p & ~(uintptr_t)15;
+  uint32_t d[17];
+  const uint32_t q = (uint32_t)((g - A4) >> 2) & 3u;
 #pragma unroll
-  for (int k = 0; k < 17; ++k) e[k] = (t[k + 1] & m1) | (t[k] & ~m1);
+  for (int j = 0; j < 4; ++j) {
+    const uintptr_t a = A4 + 16u * (uint32_t)j;
+    const bool used = head_slot_used(h, A4, g, j);
+    uint32_t x0 = used ? hd.d[4 * j + 0] : 0u, x1 = used ? hd.d[4 * j + 1] : 0u;
+    uint32_t x2 = used ? hd.d[4 * j + 2] : 0u, x3 = used ? hd.d[4 * j + 3] : 0u;
+    if (a < g) {  // (used) the slot straddling g was loaded from g: its words move up by q dwords
+      x3 = q == 1u ? x2 : (q == 2u ? x1 : x0);
+      x2 = q == 1u ? x1 : (q == 2u ? x0 : 0u);
+      x1 = q == 1u ? x0 : 0u;
+      x0 = 0u;
+    }
+    d[4 * j + 0] = x0; d[4 * j + 1] = x1; d[4 * j + 2] = x2; d[4 * j + 3] = x3;
+  }
+  d[16] = head_edge_used(h, ps, g) ? hd.d[16] : 0u;
+  const uint32_t b = (uint32_t)ps & 3u;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(e[k + 1], e[k], b);
+  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], b);
   mask_inject<16>(w, (int)(int64_t)(h.p - ps), h.s);
+}
+
+// Raw register of the round's heads from their words (every lane of a group
+// holds its head's).
+__device__ __forceinline__ uint32_t head_chain(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[16],
+                                               uint32_t nlev, int lane) {
   uint32_t crc = w[0];
 #pragma unroll
   for (int k = 0; k < 16; ++k) crc = slice4_next(lds, crc, k < 15 ? w[k + 1] : 0u, lb);
@@ -1161,27 +1359,29 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWG;
   const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wv;
   const uint64_t b0 = g.n * gw / nwaves, b1 = g.n * (gw + 1) / nwaves;
-  bool filled = false;
-  LaneBase lb = make_lane_base(lane);
-  for (uint64_t gb = b0;; gb += kWave) {
-    // (every wave reaches the workgroup barrier once, also with an empty range)
+  const LaneBase lb = make_lane_base(lane);
+  uintptr_t lp = 0;  // the lane's buffer of the current group: start, length, ~init
+  uint64_t lL = 0;
+  uint32_t ls = 0;
+  if (b0 + (uint64_t)lane < b1) g.lane_meta(b0 + (uint64_t)lane, lp, lL, ls);  // in flight during the fill
+  fill_lds<kWavesPerWG>(lds, ka.tables);
+  __syncthreads();
+  for (uint64_t gb = b0; gb < b1; gb += kWave) {
     const bool valid = gb + (uint64_t)lane < b1;
     const uint64_t i = gb + (uint64_t)lane;
-    uintptr_t lp = 0;
-    uint64_t lL = 0;
-    uint32_t ls = 0;
-    if (valid) g.lane_meta(i, lp, lL, ls);
-    if (!filled) {
-      fill_lds<kWavesPerWG>(lds, ka.tables);
-      __syncthreads();
-      filled = true;
+    if (gb != b0) {
+      lp = 0;
+      lL = 0;
+      ls = 0;
+      if (valid) g.lane_meta(i, lp, lL, ls);
     }
-    if (gb >= b1) break;
     const bool tiny = valid && lL < 4;
     const uint32_t J = chunks_for(lL);
     const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);  // first chunk's bytes
     const bool head = valid && !tiny && hl < kChunk;
     const uint32_t cls = hl <= 64u ? 0u : (hl <= 256u ? 1u : (hl <= 1024u ? 2u : 3u));
+    // what setup pulls across lanes: head bytes (< 4096) | kHeadLast << 16
+    const uint32_t hlx = (uint32_t)(hl & 0xFFFFu) | (J == 1u ? kHeadLast << 16 : 0u);
     if (tiny) {
       uint32_t l = ls;  // = ~init
       for (uint32_t k = 0; k < (uint32_t)lL; ++k) {
@@ -1214,44 +1414,64 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       const uint64_t mc = c == 0 ? m[0] : (c == 1 ? m[1] : (c == 2 ? m[2] : m[3]));
       const uint32_t per = 64u >> nlev;
       const uint32_t rank = t * per + ((uint32_t)lane >> nlev);
-      h.ok = rank < (uint32_t)__builtin_popcountll(mc);
-      const uint32_t src = h.ok ? nth_set_bit(mc, rank) : (uint32_t)lane;
+      const bool ok = rank < (uint32_t)__builtin_popcountll(mc);
+      const uint32_t src = ok ? nth_set_bit(mc, rank) : (uint32_t)lane;
       const int sa = (int)(src << 2);
       const uint32_t plo = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)lp);
       const uint32_t phi = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)(lp >> 32));
-      const uint32_t hh = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)hl);
+      const uint32_t hx = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)hlx);
       h.s = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)ls);
-      const uint32_t jj = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)J);
       h.p = ((uintptr_t)phi << 32) | plo;
-      h.ce = h.p + hh;
-      h.src = src;
-      h.last = jj == 1u;
+      h.hl = hx & 0xFFFFu;
+      h.tag = src | (ok ? kHeadOk : 0u) | (hx >> 16);
     };
     if (NR == 0) continue;
-    HeadLane hc0;
-    HeadData dc;
-    uint32_t P0, L0;
-    setup(0, hc0, P0, L0);
-    head_load(hc0, P0, lane, dc);
-    for (uint32_t R = 0; R < NR; ++R) {
-      HeadLane hn = hc0;
-      HeadData dn;
-      uint32_t P1 = P0, L1 = L0;
-      if (R + 1 < NR) {
-        setup(R + 1, hn, P1, L1);
-        head_load(hn, P1, lane, dn);
-      }
-      const uint32_t raw = head_raw(lds, lb, hc0, dc, P0, L0, lane);
-      if (hc0.ok && ((uint32_t)lane & (P0 - 1u)) == 0u) {
-        const uint64_t ib = gb + hc0.src;
-        if (hc0.last) ka.out[ib] = finish(~raw, ka.flags);
+    // Two buffers, A and B, in ping-pong: a buffer's next round is loaded
+    // right after its words are built (the registers carry over, no copies),
+    // so each round's loads have two rounds of chains to arrive.  Past the
+    // last round a buffer reloads its own round (valid addresses, unused).
+    const uintptr_t safe = (uintptr_t)ka.tables;
+    HeadLane hA, hB;
+    HeadData dA, dB;
+    uint32_t PA, LA, PB, LB;
+    setup(0, hA, PA, LA);
+    head_load(hA, PA, lane, safe, dA);
+    // (A's loads issue before B's on entry as on the back edge: the wait
+    // counts the compiler derives for the loop then let B's stay in flight)
+    asm volatile("" ::: "memory");
+    hB = hA;
+    PB = PA;
+    LB = LA;
+    if (NR > 1) setup(1, hB, PB, LB);
+    head_load(hB, PB, lane, safe, dB);
+    auto finish_round = [&](uint32_t raw, uint32_t tag, uint32_t P) {
+      if ((tag & kHeadOk) && ((uint32_t)lane & (P - 1u)) == 0u) {
+        const uint64_t ib = gb + (tag & 63u);
+        if (tag & kHeadLast) ka.out[ib] = finish(~raw, ka.flags);
         else ka.hc[ib] = raw;
       }
-      hc0 = hn;
-      dc = dn;
-      P0 = P1;
-      L0 = L1;
+    };
+    for (uint32_t R = 0; R < NR; R += 2) {
+      uint32_t w[16];
+      head_words(hA, dA, PA, lane, w);
+      uint32_t tag = hA.tag, P = PA, nl = LA;
+      if (R + 2 < NR) setup(R + 2, hA, PA, LA);
+      head_load(hA, PA, lane, safe, dA);
+      asm volatile("" ::: "memory");
+      finish_round(head_chain(lds, lb, w, nl, lane), tag, P);
+      // B's half runs even past the last round (then on its own reloaded
+      // round, not written): a branch around its loads would make the wait
+      // counts at the loop head assume the worst order
+      head_words(hB, dB, PB, lane, w);
+      tag = R + 1 < NR ? hB.tag : 0u;
+      P = PB;
+      nl = LB;
+      if (R + 3 < NR) setup(R + 3, hB, PB, LB);
+      head_load(hB, PB, lane, safe, dB);
+      asm volatile("" ::: "memory");
+      finish_round(head_chain(lds, lb, w, nl, lane), tag, P);
     }
+    // (the last reloads drain before the next group's buffers are set up)
   }
 }
 
@@ -1285,12 +1505,13 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
       return;
     }
   }
-  run_units<M, waves_of<M>()>(g, ka, lds);
+  if constexpr (M == kGeneral) run_general<waves_of<M>()>(g, ka, lds);
+  else run_units<M, waves_of<M>()>(g, ka, lds);
 }
 
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  run_units<kGeneral, kGenWaves>(g, ka, lds);
+  run_general<kGenWaves>(g, ka, lds);
 }
 
 // Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.
@@ -1651,7 +1872,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   const uint32_t* ubuf = reinterpret_cast<const uint32_t*>(lds + kUnitOff);
   const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,
                        ubuf + kUnitsPerWG, ub0};
-  run_units<kGeneral, kGenWaves>(g, ka, lds);
+  run_general<kGenWaves>(g, ka, lds);
   NVL_FSTAMP(2);
   const Rec* lr = reinterpret_cast<const Rec*>(lds + kRecOff);
   Rec* edge = reinterpret_cast<Rec*>(lds + kEdgeOff);

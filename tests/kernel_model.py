@@ -149,25 +149,37 @@ def head_class(hl: int) -> int:
 def head_raw(mem: bytes, p: int, L: int, J: int, s: int) -> int:
     """Raw register of buffer [p, p+L)'s head (partial first chunk, 1..4095
     bytes) the way head_load / head_raw run it: a group of P lanes, lane k's
-    piece [ce - 64P + 64k, +64) from the five 16-byte granules at its floor16,
-    granules outside [p, ce) not loaded."""
+    piece [ce - 64P + 64k, +64) read as four 16-byte slots from the 4-byte
+    aligned A4 at or below it plus the dword at A4 + 64; a slot wholly below
+    p's granule g is not loaded, the one straddling g is loaded from g."""
     hl = L - CHUNK * (J - 1)
     assert 4 <= hl < CHUNK or (J > 1 and 1 + OVER <= hl < CHUNK)
     ce = p + hl
+    g = p & ~15
     P = head_class(hl)
+
+    def load(a: int, n: int) -> bytes:
+        # fault safety: only 16-B granules holding bytes of [p, ce)
+        assert (a & ~15) >= g and ((a + n - 1) & ~15) <= ((ce - 1) & ~15), (a, n, p, ce)
+        return mem[a:a + n]
+
     lanes = []
     for k in range(P):
         ps = ce - 64 * P + 64 * k
-        g0 = ps & ~15
-        d = bytearray(80)
-        for j in range(5):
-            G = g0 + 16 * j
-            if G + 16 > p and G < ce:
-                # fault safety: only granules holding bytes of [p, ce)
-                assert (p & ~15) <= G <= ((ce - 1) & ~15), (G, p, ce)
-                d[16 * j:16 * j + 16] = mem[G:G + 16]
-        r = ps & 15
-        words = [int.from_bytes(d[r + 4 * q:r + 4 * q + 4], "little") for q in range(16)]
+        A4 = ps & ~3
+        d = bytearray(68)
+        for j in range(4):
+            a = A4 + 16 * j
+            if a + 16 <= g:
+                continue
+            if a < g:
+                d[16 * j + (g - a):16 * j + 16] = load(g, 16)[:16 - (g - a)]
+            else:
+                d[16 * j:16 * j + 16] = load(a, 16)
+        if ps & 3 and A4 + 68 > g:
+            d[64:68] = load(A4 + 64, 4)
+        b = ps & 3
+        words = [int.from_bytes(d[b + 4 * q:b + 4 * q + 4], "little") for q in range(16)]
         words = _mask_inject(words, p - ps, s)
         crc = 0
         for w in words:

@@ -313,10 +313,34 @@ struct KArgs {
   uint32_t* hc;
 };
 
+// floor(a / d) for wave-uniform a < 2^63, d > 0, from a double-precision
+// estimate (inv_d = 1/d, loop-invariant) corrected by a step or two: the
+// integer 64-bit division is a ~100-instruction software sequence, and the
+// general loops ran several per work unit (3.6x the aligned kernel's scalar
+// instructions, PMC SQ_INSTS_SALU).
+__device__ __forceinline__ uint64_t udiv_est(uint64_t a, uint64_t d, double inv_d) {
+  uint64_t q = (uint64_t)((double)a * inv_d);
+  while (q > 0 && q * d > a) --q;
+  while ((q + 1) * d <= a) ++q;
+  return q;
+}
+// The same with a shift when d is a power of two (the grid's unit count on
+// a 256-CU part, the chunk count of power-of-two buffers): no VALU at all.
+__device__ __forceinline__ uint64_t udiv_u(uint64_t a, uint64_t d) {
+  if ((d & (d - 1u)) == 0u) return a >> __builtin_ctzll(d);
+  return udiv_est(a, d, 1.0 / (double)d);
+}
+
 // Global work units: the grid's NU = gridDim.x * kUnitsPerWG units split the
 // chunk space [0, T) evenly; workgroup b owns units [64b, 64b+64).
+// F: the estimate-based division (general kernels); the aligned kernel keeps
+// the integer one, whose code needs no vector registers (with the estimate's
+// double arithmetic in its loop it spilled 23 VGPRs).
+template <bool F>
 __device__ __forceinline__ uint64_t global_unit_lo(uint64_t T, uint32_t u) {
-  return T * (uint64_t)u / ((uint64_t)gridDim.x * kUnitsPerWG);
+  const uint64_t nu = (uint64_t)gridDim.x * kUnitsPerWG;
+  if constexpr (F) return udiv_u(T * (uint64_t)u, nu);
+  else return T * (uint64_t)u / nu;
 }
 __device__ __forceinline__ void global_put_recs(const KArgs& ka, uint32_t u, const Rec& h, const Rec& t) {
   if (ka.recs) {
@@ -332,16 +356,19 @@ struct FixedGeom {
   const uint32_t* init;
   uint32_t init_all;
   __device__ __forceinline__ uint64_t total() const { return n * (uint64_t)J; }
+  template <bool F = false>
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
-    i = t / J;
+    if constexpr (F) i = udiv_u(t, J);
+    else i = t / J;
     c = (uint32_t)(t - i * J);
   }
   __device__ __forceinline__ BufInfo info(uint64_t i) const {
     const uint32_t ini = init ? ldc(init, i) : init_all;
     return BufInfo{base + i * stride, len, J, ~ini};
   }
+  template <bool F>
   __device__ __forceinline__ void locate_unit(uint32_t, uint64_t t, uint64_t& i, uint32_t& c) const {
-    locate(t, i, c);
+    locate<F>(t, i, c);
   }
   // Buffer i's start, length and ~init in this lane (head kernel).
   __device__ __forceinline__ void lane_meta(uint64_t i, uintptr_t& p, uint64_t& L, uint32_t& sx) const {
@@ -349,7 +376,8 @@ struct FixedGeom {
     L = len;
     sx = ~(init ? init[i] : init_all);
   }
-  __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo(T, u); }
+  template <bool F>
+  __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo<F>(T, u); }
   __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
     global_put_recs(ka, u, h, t);
   }
@@ -375,6 +403,7 @@ struct VarGeom {
     c = (uint32_t)(t - chunk_start[lo]);
   }
   // Start of work unit u (chunk t = its first): one load instead of a search.
+  template <bool F>
   __device__ __forceinline__ void locate_unit(uint32_t u, uint64_t t, uint64_t& i, uint32_t& c) const {
     i = ldc(unit_first, u);
     c = (uint32_t)(t - ldc(chunk_start, i));
@@ -389,7 +418,8 @@ struct VarGeom {
     L = lengths[i];
     sx = ~(init ? init[i] : init_all);
   }
-  __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo(T, u); }
+  template <bool F>
+  __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo<F>(T, u); }
   __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
     global_put_recs(ka, u, h, t);
   }
@@ -726,10 +756,10 @@ struct Pos {
   BufInfo bi;
 };
 
-template <class G>
+template <bool F, class G>
 __device__ __forceinline__ Pos unit_start_pos(const G& g, uint32_t u, uint64_t t) {
   Pos p;
-  g.locate_unit(u, t, p.i, p.c);
+  g.template locate_unit<F>(u, t, p.i, p.c);
   p.bi = g.info(p.i);
   return p;
 }
@@ -938,7 +968,8 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t T = g.total();
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
-  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.unit_lo(T, uu); };
+  constexpr bool kFastDiv = M != kAligned;
+  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.template unit_lo<kFastDiv>(T, uu); };
   // kGeneral: a head chunk (partial first chunk, or a buffer of < 4 bytes)
   // belongs to crc32c_head_kernel: the step that reaches one loads and
   // computes nothing; its raw register hc[i] is prefetched with the buffer's
@@ -963,7 +994,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   Chunk c0, c1;
   uint32_t hv0 = 0u;
   if (t < t1) {  // the first step's loads overlap the LDS fill
-    p0 = unit_start_pos(g, u, t);
+    p0 = unit_start_pos<kFastDiv>(g, u, t);
     if (!skip(p0)) load_chunk<M>(p0.bi, p0.c, lane, c0);
     hv0 = hc_of(p0);
     if (kStep == 2 && t + 1 < t1) {
@@ -995,7 +1026,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
         q1v = true;
       }
     } else if (un_lo < un_hi) {  // the next unit's first step
-      q0 = unit_start_pos(g, un, un_lo);
+      q0 = unit_start_pos<kFastDiv>(g, un, un_lo);
       q0v = true;
       if (kStep == 2 && un_lo + 1 < un_hi) {
         q1 = next_pos(g, q0);
@@ -1110,7 +1141,7 @@ __device__ __forceinline__ void run_units_pp(const G& g, const KArgs& ka, uint8_
   const uint64_t T = g.total();
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
   const uintptr_t safe = (uintptr_t)ka.tables;  // >= 4100 valid bytes
-  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.unit_lo(T, uu); };
+  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.template unit_lo<true>(T, uu); };
   auto first_body = [&](const Pos& q) -> uint32_t { return head_first(q.bi.len) ? 1u : 0u; };
   const Rec none{kNoBuf, 0u, 0u};
 
@@ -1139,7 +1170,7 @@ __device__ __forceinline__ void run_units_pp(const G& g, const KArgs& ka, uint8_
     sl.u = gu;
     sl.start = fresh;
     sl.end = gt + 1 == gt1;
-    sl.pos = fresh ? unit_start_pos(g, gu, gt) : next_pos(g, last);
+    sl.pos = fresh ? unit_start_pos<true>(g, gu, gt) : next_pos(g, last);
     sl.work = !(sl.pos.c == 0 && head_first(sl.pos.bi.len));
     last = sl.pos;
     fresh = sl.end;
@@ -1705,9 +1736,11 @@ struct VarGeomFused {
   const uint32_t* uc;     // LDS: that chunk's index within the buffer
   uint32_t ub0;
   __device__ __forceinline__ uint64_t total() const { return C1 - C0; }
+  template <bool F>
   __device__ __forceinline__ uint64_t unit_lo(uint64_t span, uint32_t u) const {
     return C0 + span * (uint64_t)(u - ub0) / kUnitsPerWG;
   }
+  template <bool F>
   __device__ __forceinline__ void locate_unit(uint32_t u, uint64_t, uint64_t& i, uint32_t& c) const {
     i = ubuf[u - ub0];
     c = uc[u - ub0];

@@ -862,7 +862,7 @@ __device__ unsigned long long g_stamps[4 * 65536];
 #endif
 constexpr uint32_t kTail = NVL_TAIL;
 
-template <int U, int NW = kWavesPerWG>
+template <int U, int NW = kWavesPerWG, int M = kAligned>
 __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
@@ -891,7 +891,7 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
 #pragma unroll
   for (int k = 0; k < U; ++k) {
     ok[k] = unit_pos(u, k, gp[k]);
-    if (ok[k]) load_chunk<kAligned>(gp[k].bi, 0, lane, cur[k]);
+    if (ok[k]) load_chunk<M>(gp[k].bi, 0, lane, cur[k]);
   }
   fill_lds<NW>(lds, ka.tables);
   __syncthreads();
@@ -907,7 +907,7 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       nok[k] = unit_pos(un, k, np[k]);
-      if (nok[k]) load_chunk<kAligned>(np[k].bi, 0, lane, nxt[k]);
+      if (nok[k]) load_chunk<M>(np[k].bi, 0, lane, nxt[k]);
     }
     if (ok[U - 1]) {  // full unit
       BufInfo bis[U];
@@ -917,7 +917,7 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
         bis[k] = gp[k].bi;
         cs[k] = 0;
       }
-      group_raw<kAligned, U>(lds, lb, bis, cs, lane, cur, raws);
+      group_raw<M, U>(lds, lb, bis, cs, lane, cur, raws);
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < U; ++k) ka.out[gp[k].i] = finish(~raws[k], ka.flags);
@@ -926,7 +926,7 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         if (ok[k]) {
-          const uint32_t r = chunk_raw<kAligned>(lds, lb, gp[k].bi, 0, lane, cur[k]);
+          const uint32_t r = chunk_raw<M>(lds, lb, gp[k].bi, 0, lane, cur[k]);
           if (lane == 0) ka.out[gp[k].i] = finish(~r, ka.flags);
         }
       }
@@ -1536,6 +1536,19 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
       return;
     }
   }
+#ifndef NVL_GEN_PAIR_U
+#define NVL_GEN_PAIR_U 2  // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 91.7 through run_units)
+#endif
+#if !defined(NVL_GEN_NO_PAIRS)
+  if constexpr (M == kGeneral) {
+    // one whole chunk per buffer (len == 4096, any alignment): scheduler A,
+    // one buffer per unit, no records
+    if (g.J == 1 && !head_first(g.len)) {
+      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
+      return;
+    }
+  }
+#endif
   if constexpr (M == kGeneral) run_general<waves_of<M>()>(g, ka, lds);
   else run_units<M, waves_of<M>()>(g, ka, lds);
 }

@@ -175,20 +175,23 @@ DeviceState* current_state(int* rc) {
 }
 
 // Variable-batch workspace: [counts n+1][chunk_start n+1][unit map][records][head contributions n][scan scratch]
+// [chunk counts][chunk_start][unit map][records][hc][flags: long_bufs][scan temp]
 size_t batch_ws_layout(uint64_t n, int num_cu, size_t* off_cs, size_t* off_map, size_t* off_recs, size_t* off_hc,
-                       size_t* off_tmp) {
+                       size_t* off_flags, size_t* off_tmp) {
   const size_t cnt = align_up((n + 1) * sizeof(uint64_t), 256);
   const size_t cs = cnt;
   const size_t map = align_up(var_unit_map_bytes(num_cu), 256);
   const size_t recs = align_up(var_recs_bytes(num_cu), 256);
   const size_t hc = align_up(n * sizeof(uint32_t), 256);
+  const size_t fl = 256;
   const size_t tmp = align_up(scan_temp_bytes(n + 1), 256);
   *off_cs = cnt;
   *off_map = cnt + cs;
   *off_recs = cnt + cs + map;
   *off_hc = cnt + cs + map + recs;
-  *off_tmp = cnt + cs + map + recs + hc;
-  return cnt + cs + map + recs + hc + tmp;
+  *off_flags = cnt + cs + map + recs + hc;
+  *off_tmp = cnt + cs + map + recs + hc + fl;
+  return cnt + cs + map + recs + hc + fl + tmp;
 }
 
 size_t fixed_ws_bytes(uint64_t len, uint64_t n, int num_cu) { return fixed_recs_bytes(num_cu, len, n); }
@@ -222,8 +225,8 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out) return NVL_CRC32C_EINVAL;
   if (n >= (1ull << 31) - 2) return NVL_CRC32C_EINVAL;
-  size_t off_cs, off_map, off_recs, off_hc, off_tmp;
-  const size_t need = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_tmp);
+  size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
+  const size_t need = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
   bool own = false;
   if (!ws) {
     if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
@@ -237,6 +240,7 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   uint64_t* unit_first = reinterpret_cast<uint64_t*>(w + off_map);
   Rec* recs = reinterpret_cast<Rec*>(w + off_recs);
   uint32_t* hc = reinterpret_cast<uint32_t*>(w + off_hc);
+  uint32_t* long_bufs = reinterpret_cast<uint32_t*>(w + off_flags);
   void* tmp = w + off_tmp;
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   const bool small = var_plan_small(n);
@@ -251,14 +255,14 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
 #endif
   hipError_t e;
   if (small) {
-    e = launch_var_plan_small(lc, lengths, n, cs, unit_first);
+    e = launch_var_plan_small(lc, lengths, n, cs, unit_first, long_bufs);
   } else {
-    e = launch_var_counts(lengths, n, cnt, st);
+    e = launch_var_counts(lengths, n, cnt, long_bufs, st);
     if (e == hipSuccess) e = exclusive_scan_u64(tmp, need - off_tmp, cnt, cs, n + 1, st);
   }
   if (e == hipSuccess)
     e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, unit_first, n, init, init_all, out,
-                   flags, recs, hc, small);
+                   flags, recs, hc, long_bufs, small);
   if (own) (void)hipFreeAsync(ws, st);
   return hip_rc(e);
 }
@@ -533,7 +537,8 @@ size_t nvl_crc32c_batch_workspace_bytes(uint64_t n) {
   int rc = NVL_CRC32C_OK;
   DeviceState* s = current_state(&rc);
   size_t a, b, c, d, e;
-  return batch_ws_layout(n, s ? s->num_cu : 256, &a, &b, &c, &d, &e);
+  size_t f;
+  return batch_ws_layout(n, s ? s->num_cu : 256, &a, &b, &c, &d, &f, &e);
 }
 
 int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
@@ -604,8 +609,8 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   hipStream_t st = thread_stream(s->device);
   if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
-  size_t off_cs, off_map, off_recs, off_hc, off_tmp;
-  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_tmp);
+  size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
+  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
   const size_t dbytes = total + n * 4 + ws + 512;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
@@ -678,8 +683,8 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   hipStream_t st = thread_stream(s->device);
   if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
-  size_t off_cs, off_map, off_recs, off_hc, off_tmp;
-  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_tmp);
+  size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
+  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
   const size_t dbytes = align_up(total, 256) + align_up(n * 4, 256) + ws + 256;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));

@@ -55,15 +55,19 @@ size_t var_unit_map_bytes(int num_cu);                           // unit map par
 // Plan for the variable-length kernel: small batches in one launch
 // (chunk_start + unit map), large ones as counts -> device scan -> unit map.
 bool var_plan_small(uint64_t n);
+// long_bufs: one u32 of workspace, set by the plan (0: every buffer has at
+// most 32 chunks, so the body kernel can give each buffer to one wave).
 hipError_t launch_var_plan_small(const LaunchCtx& lc, const uint64_t* lengths, uint64_t n, uint64_t* chunk_start,
-                                 uint64_t* unit_first);
-hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st);
+                                 uint64_t* unit_first, uint32_t* long_bufs);
+hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, uint32_t* long_bufs,
+                             hipStream_t st);
 // have_unit_map: unit_first already written (small plan); otherwise built here.
 // hc: n u32 of workspace (head contributions, written by the head kernel
 // that every variable-length call launches first).
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
-                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, bool have_unit_map);
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, uint32_t* long_bufs,
+                      bool have_unit_map);
 
 // Plan + checksum + fix-up in one launch (n <= kPlanSmallMax, lc.counter
 // set); recs: the launch_var workspace records (hold the edge records).

@@ -311,6 +311,10 @@ struct KArgs {
   // before the body kernel runs (only read for such buffers); nullptr when no
   // buffer of the batch has one.
   uint32_t* hc;
+  // Variable-length batches: nonzero when some buffer has more than
+  // kBufsMaxJ chunks (set by the plan kernels); zero lets the body kernel use
+  // the buffer scheduler (no split buffers).  nullptr: unknown.
+  const uint32_t* long_bufs = nullptr;
 };
 
 // floor(a / d) for wave-uniform a < 2^63, d > 0, from a double-precision
@@ -509,11 +513,19 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
     // byte ce-1), lane 0 when the chunk has an overhang (chunk 0 starting
     // after p: the 16 bytes below A4, clamped up to p's granule; build_words
     // moves them into place).
-    const bool ovh = kOver > 0 && c == 0 && A4 + r > (uintptr_t)bi.p;
-    if ((lane == 63 && r != 0) || (lane == 0 && ovh)) {
-      const uintptr_t ea = lane == 63 ? A4 + kChunk - 12u : (A4 - 16u > g ? A4 - 16u : g);
-      const u32x4 v = ld16(ea);
-      ch.e[0] = v.x; ch.e[1] = v.y; ch.e[2] = v.z; ch.e[3] = v.w;
+    if constexpr (kOver == 0) {
+      // r != 0: the dword past the last piece (it holds byte ce-1); r == 0:
+      // the chunk's last dword (unused).  Every lane loads it (one line, no
+      // branch around the load: the wait counts stay exact).
+      (void)g;
+      ch.e[3] = *(const __attribute__((address_space(1))) uint32_t*)(A4 + (r ? kChunk : kChunk - 4u));
+    } else {
+      const bool ovh = c == 0 && A4 + r > (uintptr_t)bi.p;
+      if ((lane == 63 && r != 0) || (lane == 0 && ovh)) {
+        const uintptr_t ea = lane == 63 ? A4 + kChunk - 12u : (A4 - 16u > g ? A4 - 16u : g);
+        const u32x4 v = ld16(ea);
+        ch.e[0] = v.x; ch.e[1] = v.y; ch.e[2] = v.z; ch.e[3] = v.w;
+      }
     }
   }
 }
@@ -1251,6 +1263,140 @@ __device__ __forceinline__ void run_general(const G& g, const KArgs& ka, uint8_t
 }
 
 // ---------------------------------------------------------------------------
+// Scheduler C -- variable-length batches whose buffers are all short (at most
+// kBufsMaxJ chunks).  Workgroup b owns the buffers that START in its chunk
+// range [T*b/G, T*(b+1)/G) (balanced to within one buffer), so no buffer is
+// split: no records, no fix-up.  Its waves claim groups of consecutive
+// buffers from the LDS counter, one buffer per lane (offset, length, ~init in
+// the lane's registers: no scalar loads per buffer), and walk each buffer's
+// body chunks (a head chunk is crc32c_head_kernel's: its raw register enters
+// with the first body chunk).  As in scheduler A the next chunk's loads go
+// out before the current chunk's words are built; the unit scheduler (B),
+// which also splits buffers across waves, ran the same chunks ~30 % slower
+// (fixed-stride: 91.7 vs 70.4 us for 10^5 x 4096 B).
+constexpr uint32_t kBufsMaxJ = 32;
+
+template <int NW, class G>
+__device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* lds, uint64_t i0, uint64_t i1) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nb = i1 > i0 ? i1 - i0 : 0;
+  const uint32_t GS = (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (4u * NW)));  // buffers per group
+  const uint64_t ngroups = (nb + GS - 1) / GS;
+  const uintptr_t safe = (uintptr_t)ka.tables;
+
+  // the current group: lane j holds buffer gb + j (j < gn).  (Loading the
+  // next group's metadata one group ahead measured slower: 95 -> 101 us on
+  // 10^5 x 4097 B, the copies at adoption wait on the loads in flight.)
+  uint64_t gb = 0;
+  uintptr_t lp = 0;
+  uint64_t lL = 0;
+  uint32_t ls = 0;
+  uint64_t todo = 0;  // group lanes whose buffers have body chunks and are not started yet
+  bool synced = false, done = false;
+  auto load_group = [&](uint64_t k) {
+    gb = i0 + k * GS;
+    const uint32_t gn = (uint32_t)min<uint64_t>(GS, i1 - gb);
+    g.lane_meta(gb + (uint64_t)min<uint32_t>((uint32_t)lane, gn - 1u), lp, lL, ls);  // (every lane loads)
+    const bool body = (uint32_t)lane < gn && chunks_for(lL) > (head_first(lL) ? 1u : 0u);
+    todo = __ballot(body);
+  };
+  // claim groups until one has a body buffer (false: none left)
+  auto claim = [&]() -> bool {
+    while (todo == 0) {
+      if (done || !synced) return false;
+      const uint32_t k = pull_unit(lds, lane);
+      if (k >= ngroups) {
+        done = true;
+        return false;
+      }
+      load_group(k);
+    }
+    return true;
+  };
+  struct BPos {
+    BufInfo bi;
+    uint64_t i;
+    uint32_t c, fb;
+    bool valid;
+  };
+  auto start_buffer = [&](BPos& q) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+    todo &= todo - 1u;
+    const uintptr_t p = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lp >> 32), (int)j) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lp, (int)j);
+    const uint64_t L = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lL >> 32), (int)j) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lL, (int)j);
+    const uint32_t sx = (uint32_t)__builtin_amdgcn_readlane((int)ls, (int)j);
+    q.bi = BufInfo{reinterpret_cast<const uint8_t*>(p), L, chunks_for(L), sx};
+    q.i = gb + j;
+    q.fb = head_first(L) ? 1u : 0u;
+    q.c = q.fb;
+    q.valid = true;
+  };
+  auto advance = [&](const BPos& cur, BPos& nx) {
+    nx = cur;
+    if (cur.valid && cur.c + 1u < cur.bi.J) {
+      nx.c = cur.c + 1u;
+      return;
+    }
+    nx.valid = false;
+    if (todo != 0 || claim()) start_buffer(nx);
+  };
+  // the chunk's loads, and hc[i] with a head-first buffer's first body chunk
+  // (every lane, every time: past the end they read the table blob)
+  auto load = [&](const BPos& q, Chunk& ch, uint32_t& hv) {
+    if (q.valid) {
+      load_chunk<kGeneral>(q.bi, q.c, lane, ch);
+    } else {
+      BufInfo sb{reinterpret_cast<const uint8_t*>(safe), kChunk, 1u, 0u};
+      load_chunk<kGeneral>(sb, 0, lane, ch);
+    }
+    const bool hu = q.valid && ka.hc && q.fb == 1u && q.c == 1u;
+    hv = __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)(hu ? (uintptr_t)(ka.hc + q.i)
+                                                                                           : safe));
+  };
+
+  BPos cur{};
+  cur.valid = false;
+  Chunk C;
+  uint32_t hvC = 0u;
+  if (wv < ngroups) {  // the pre-assigned first group (fill_lds starts the counter at NW)
+    load_group(wv);
+    if (todo) start_buffer(cur);
+  }
+  load(cur, C, hvC);  // overlaps the LDS fill
+  fill_lds<NW>(lds, ka.tables);
+  __syncthreads();
+  synced = true;
+  const LaneBase lb = make_lane_base(lane);
+  if (!cur.valid) {
+    BPos z{};
+    z.valid = false;
+    advance(z, cur);
+    load(cur, C, hvC);
+  }
+  uint32_t acc = 0u;
+  while (cur.valid) {
+    BPos nx;
+    advance(cur, nx);
+    Chunk N;
+    uint32_t hvN;
+    load(nx, N, hvN);
+    uint32_t w[16], ov[4];
+    build_words<kGeneral>(cur.bi, cur.c, lane, C, w, ov);
+    const uint32_t raw = chain_fold<kGeneral>(lds, lb, w, lane);
+    const bool first = cur.c == cur.fb;
+    const bool head_in = first && cur.fb == 1u && ka.hc;
+    acc = (!first || head_in) ? shift4096(lds, first ? hvC : acc, lane) ^ raw : raw;
+    if (cur.c + 1u == cur.bi.J && lane == 0) ka.out[cur.i] = finish(~acc, ka.flags);
+    cur = nx;
+    C = N;
+    hvC = hvN;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Head chunks -- crc32c_head_kernel, launched before the kGeneral body
 // kernel of the same batch.  A head is a buffer's partial first chunk, h =
 // 1..4095 bytes (the whole buffer when it has one chunk).  The chunk pass
@@ -1553,19 +1699,44 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
   else run_units<M, waves_of<M>()>(g, ka, lds);
 }
 
+#ifndef NVL_VAR_BUFS
+#define NVL_VAR_BUFS 1  // 1: scheduler C when every buffer has <= kBufsMaxJ chunks
+#endif
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  if (NVL_VAR_BUFS && ka.long_bufs && ldc(ka.long_bufs, 0) == 0u) {
+    // Workgroup b: the buffers that start in its chunk range [lo(64b),
+    // lo(64b+64)): unit_first[u] holds the buffer containing chunk lo(u),
+    // which starts there or earlier (then it is the previous workgroup's).
+    const uint64_t T = g.total();
+    const uint32_t ub0 = blockIdx.x * kUnitsPerWG, nu = gridDim.x * kUnitsPerWG;
+    auto first_at = [&](uint32_t u) -> uint64_t {
+      if (u >= nu) return g.n;
+      const uint64_t lo = global_unit_lo<true>(T, u);
+      if (lo >= T) return g.n;
+      const uint64_t b = ldc(g.unit_first, u);
+      return ldc(g.chunk_start, b) == lo ? b : b + 1u;
+    };
+    const uint64_t i0 = first_at(ub0), i1 = first_at(ub0 + kUnitsPerWG);
+    if (threadIdx.x < kUnitsPerWG && ka.recs) {  // no split buffers: empty records for the fix-up
+      ka.recs[2ull * (ub0 + threadIdx.x)] = Rec{kNoBuf, 0u, 0u};
+      ka.recs[2ull * (ub0 + threadIdx.x) + 1] = Rec{kNoBuf, 0u, 0u};
+    }
+    run_bufs<kGenWaves>(g, ka, lds, i0, i1);
+    return;
+  }
   run_general<kGenWaves>(g, ka, lds);
 }
 
 // Per-buffer chunk counts for the variable-length plan: cnt[i] = J_i, cnt[n] = 0.
 __global__ void crc32c_var_counts(const uint64_t* __restrict__ lengths, uint64_t n,
-                                  uint64_t* __restrict__ cnt) {
+                                  uint64_t* __restrict__ cnt, uint32_t* __restrict__ long_bufs) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     cnt[i] = chunks_for(lengths[i]);
   } else if (i == n) {
     cnt[i] = 0;
+    *long_bufs = 0u;  // (crc32c_unit_map, two launches later, sets it)
   }
 }
 
@@ -1573,11 +1744,12 @@ __global__ void crc32c_var_counts(const uint64_t* __restrict__ lengths, uint64_t
 // buffer i owns the units u with cs_i <= floor(T*u/NU) < cs_{i+1}, i.e.
 // u in [ceil(cs_i*NU/T), ceil(cs_{i+1}*NU/T)).
 __global__ void crc32c_unit_map(const uint64_t* __restrict__ cs, uint64_t n, uint64_t NU,
-                                uint64_t* __restrict__ unit_first) {
+                                uint64_t* __restrict__ unit_first, uint32_t* __restrict__ long_bufs) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t T = cs[n];
   const uint64_t a = cs[i], b = cs[i + 1];
+  if (b - a > kBufsMaxJ) *long_bufs = 1u;  // (every writer stores the same value)
   uint64_t u0 = (a * NU + T - 1) / T, u1 = (b * NU + T - 1) / T;
   if (u1 > NU) u1 = NU;
   for (uint64_t u = u0; u < u1; ++u) unit_first[u] = i;
@@ -1605,7 +1777,8 @@ __device__ __forceinline__ uint32_t plan_pad(uint32_t i) { return i + (i >> 5); 
 
 __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t* __restrict__ lengths, uint64_t n,
                                                                 uint64_t NU, uint64_t* __restrict__ cs,
-                                                                uint64_t* __restrict__ unit_first) {
+                                                                uint64_t* __restrict__ unit_first,
+                                                                uint32_t* __restrict__ long_bufs) {
   __shared__ uint32_t js[kPlanSmallMax + kPlanSmallMax / 32];  // chunk counts, then run-relative prefixes
   __shared__ uint64_t wsum[kPlanThreads / kWave];
   __shared__ uint64_t rstart[kPlanThreads];  // first chunk of each thread's run
@@ -1619,13 +1792,17 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t
       const uint32_t i = t + (uint32_t)k * (uint32_t)kPlanThreads;
       Ls[k] = i < nn ? lengths[i] : 0;
     }
+    bool lng = false;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = t + (uint32_t)k * (uint32_t)kPlanThreads;
-      if (i < nn) js[plan_pad(i)] = chunks_for(Ls[k]);
+      const uint32_t J = chunks_for(Ls[k]);
+      lng |= J > kBufsMaxJ;
+      if (i < nn) js[plan_pad(i)] = J;
     }
+    const int any = __syncthreads_or(lng ? 1 : 0);
+    if (t == 0) *long_bufs = any ? 1u : 0u;
   }
-  __syncthreads();
   const uint32_t per = (nn + (uint32_t)kPlanThreads - 1) / (uint32_t)kPlanThreads;
   const uint32_t i0 = min(nn, t * per), i1 = min(nn, i0 + per);
   // The run's counts become run-relative exclusive prefixes in place (u32: a
@@ -2145,23 +2322,25 @@ hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint
 }
 
 hipError_t launch_var_plan_small(const LaunchCtx& lc, const uint64_t* lengths, uint64_t n, uint64_t* chunk_start,
-                                 uint64_t* unit_first) {
+                                 uint64_t* unit_first, uint32_t* long_bufs) {
   const uint64_t NU = (uint64_t)lc.num_cu * dev::kUnitsPerWG;
   hipLaunchKernelGGL(dev::crc32c_plan_small, dim3(1), dim3((uint32_t)dev::kPlanThreads), 0, lc.stream, lengths, n, NU,
-                     chunk_start, unit_first);
+                     chunk_start, unit_first, long_bufs);
   return hipGetLastError();
 }
 
-hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, hipStream_t st) {
+hipError_t launch_var_counts(const uint64_t* lengths, uint64_t n, uint64_t* cnt, uint32_t* long_bufs,
+                             hipStream_t st) {
   const uint32_t tpb = 256;
   const uint64_t blocks = (n + 1 + tpb - 1) / tpb;
-  hipLaunchKernelGGL(dev::crc32c_var_counts, dim3((uint32_t)blocks), dim3(tpb), 0, st, lengths, n, cnt);
+  hipLaunchKernelGGL(dev::crc32c_var_counts, dim3((uint32_t)blocks), dim3(tpb), 0, st, lengths, n, cnt, long_bufs);
   return hipGetLastError();
 }
 
 hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                       const uint64_t* chunk_start, uint64_t* unit_first, uint64_t n, const uint32_t* init,
-                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, bool have_unit_map) {
+                      uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, uint32_t* long_bufs,
+                      bool have_unit_map) {
   if (n == 0) return hipSuccess;
   {
     const dev::VarGeom gh{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
@@ -2172,12 +2351,12 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
   const uint64_t NU = (uint64_t)grid * dev::kUnitsPerWG;
   if (!have_unit_map) {
     hipLaunchKernelGGL(dev::crc32c_unit_map, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, lc.stream, chunk_start,
-                       n, NU, unit_first);
+                       n, NU, unit_first, long_bufs);
     hipError_t e0 = hipGetLastError();
     if (e0 != hipSuccess) return e0;
   }
   dev::VarGeom g{base, offsets, lengths, chunk_start, unit_first, n, init, init_all};
-  dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc};
+  dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc, long_bufs};
   hipLaunchKernelGGL(dev::crc32c_var_kernel, dim3(grid), dim3(dev::kWave * dev::kGenWaves), 0, lc.stream, g, ka);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -1281,7 +1281,12 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nb = i1 > i0 ? i1 - i0 : 0;
-  const uint32_t GS = (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (4u * NW)));  // buffers per group
+#ifndef NVL_BUFS_STATIC
+#define NVL_BUFS_STATIC 0  // 1: wave w takes groups w, w+NW, ... (contiguous, no claims)
+#endif
+  const uint32_t GS = NVL_BUFS_STATIC
+                          ? (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, (nb + NW - 1) / NW))
+                          : (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (4u * NW)));  // buffers per group
   const uint64_t ngroups = (nb + GS - 1) / GS;
   const uintptr_t safe = (uintptr_t)ka.tables;
 
@@ -1302,10 +1307,11 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
     todo = __ballot(body);
   };
   // claim groups until one has a body buffer (false: none left)
+  uint64_t mygrp = wv;
   auto claim = [&]() -> bool {
     while (todo == 0) {
       if (done || !synced) return false;
-      const uint32_t k = pull_unit(lds, lane);
+      const uint64_t k = NVL_BUFS_STATIC ? (mygrp += NW) : (uint64_t)pull_unit(lds, lane);
       if (k >= ngroups) {
         done = true;
         return false;
@@ -1959,7 +1965,8 @@ __device__ unsigned long long g_fstamps[8 * 1024];
 // C0/C1 (returned) bound the workgroup's chunk range.
 template <int NW>
 __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restrict__ lengths, uint32_t nn,
-                                           uint64_t& C0, uint64_t& C1) {
+                                           uint64_t& C0, uint64_t& C1, bool& long_bufs, uint64_t& B0,
+                                           uint64_t& B1) {
   constexpr uint32_t kT = kWave * NW;
   static_assert(kT <= 1024 && kPlanSmallMax % kT == 0, "plan layout assumes <= 1024 threads");
   constexpr int kPer = (int)(kPlanSmallMax / kT);
@@ -1976,13 +1983,16 @@ __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restr
       const uint32_t i = t + (uint32_t)k * kT;
       Ls[k] = i < nn ? lengths[i] : 0;
     }
+    bool lng = false;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t i = t + (uint32_t)k * kT;
-      if (i < nn) js[plan_pad(i)] = chunks_for(Ls[k]);
+      const uint32_t J = chunks_for(Ls[k]);
+      lng |= J > kBufsMaxJ;
+      if (i < nn) js[plan_pad(i)] = J;
     }
+    long_bufs = __syncthreads_or(lng ? 1 : 0) != 0;
   }
-  __syncthreads();
   NVL_FSTAMP(4);
   const uint32_t per = (nn + kT - 1) / kT;
   const uint32_t i0 = min(nn, t * per), i1 = min(nn, i0 + per);
@@ -2042,6 +2052,15 @@ __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restr
       uc[t] = (uint32_t)(q - cs);
     }
   }
+  // scheduler C: the buffers that start in [C0, C1) (every lane the same)
+  auto first_from = [&](uint64_t q) -> uint64_t {
+    if (q >= T) return nn;
+    uint64_t cs;
+    const uint32_t b = buf_of(q, cs);
+    return cs == q ? b : b + 1u;
+  };
+  B0 = long_bufs ? 0 : first_from(C0);
+  B1 = long_bufs ? 0 : first_from(C1);
   __syncthreads();
 }
 
@@ -2084,8 +2103,9 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes];
   NVL_FSTAMP(0);
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
-  uint64_t C0, C1;
-  fused_plan<kGenWaves>(lds, gv.lengths, (uint32_t)gv.n, C0, C1);
+  uint64_t C0, C1, B0, B1;
+  bool long_bufs;
+  fused_plan<kGenWaves>(lds, gv.lengths, (uint32_t)gv.n, C0, C1, long_bufs, B0, B1);
   // The range is uniform, but the 64-bit divisions that made it ran on the
   // VALU: pin it to SGPRs, or it stays in VGPRs through the main loop and
   // that spills (25 VGPRs, 108 B/lane scratch, cfg3 287 -> 430 us).
@@ -2095,7 +2115,14 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   const uint32_t* ubuf = reinterpret_cast<const uint32_t*>(lds + kUnitOff);
   const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,
                        ubuf + kUnitsPerWG, ub0};
-  run_general<kGenWaves>(g, ka, lds);
+  if (NVL_VAR_BUFS && !long_bufs) {
+    // whole buffers: no unit records, so no edge records either
+    Rec* lr0 = reinterpret_cast<Rec*>(lds + kRecOff);
+    if (threadIdx.x < 2 * kUnitsPerWG) lr0[threadIdx.x] = Rec{kNoBuf, 0u, 0u};
+    run_bufs<kGenWaves>(gv, ka, lds, uniform_u64(B0), uniform_u64(B1));
+  } else {
+    run_general<kGenWaves>(g, ka, lds);
+  }
   NVL_FSTAMP(2);
   const Rec* lr = reinterpret_cast<const Rec*>(lds + kRecOff);
   Rec* edge = reinterpret_cast<Rec*>(lds + kEdgeOff);

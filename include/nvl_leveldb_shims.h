@@ -25,11 +25,30 @@ namespace nvl {
 namespace shims {
 
 // ---------------------------------------------------------------------------
-// log::Reader over a log image held in memory (the whole file, or its part
-// from block offset 0).  The first ReadRecord scans the image once -- every
-// physical record's checksum in one batch -- and the record-level state
-// machine of log_reader.cc:62-175 then replays the scan.  Corruption reports
-// carry the reference's byte counts and reason strings.
+// The input of a streaming LogReader: leveldb::SequentialFile's contract
+// (include/leveldb/env.h, SequentialFile::Read/Skip).  Read fills up to n
+// bytes at buf and returns how many it read; a short read means the end of
+// the file.  On failure it sets *error to the Status text (e.g. "IO error:
+// ...") and returns the bytes it did read before the failure.
+class LogSource {
+ public:
+  virtual ~LogSource() {}
+  virtual size_t Read(size_t n, char* buf, std::string* error) = 0;
+  virtual bool Skip(uint64_t n, std::string* error) = 0;
+};
+
+// log::Reader.  Two inputs:
+//   * an image held in memory (the whole file, or its part from block offset
+//     0): the first ReadRecord scans it once -- every physical record's
+//     checksum in one batch;
+//   * a LogSource read in windows of `window_blocks` kBlockSize pieces (the
+//     reference reads one piece at a time, log_reader.cc:199-218): each
+//     window's checksums go in one batch, so a file larger than memory, or
+//     one still being written, is read as the reference reads it.
+// The record-level state machine of log_reader.cc:62-175 then replays the
+// scan.  Corruption reports carry the reference's byte counts and reason
+// strings; a failed read is reported as the reference's ReportDrop(kBlockSize,
+// status) (:205-211), through Reporter::Drop.
 class LogReader {
  public:
   // log_reader.h:22-30 (the reason is the text of the Status::Corruption).
@@ -37,6 +56,9 @@ class LogReader {
    public:
     virtual ~Reporter() {}
     virtual void Corruption(size_t bytes, const char* reason) = 0;
+    // A drop whose Status is not a Corruption (a failed read or skip of a
+    // streaming source): `status` is its full text.
+    virtual void Drop(size_t bytes, const char* status) { Corruption(bytes, status); }
   };
 
   // log_reader.h:32-44.  `file` must stay live while the reader is used;
@@ -45,6 +67,22 @@ class LogReader {
             uint32_t flags = 0)
       : file_(file),
         file_len_(file_len),
+        src_(nullptr),
+        window_blocks_(0),
+        reporter_(reporter),
+        checksum_(checksum),
+        flags_(flags),
+        initial_offset_(initial_offset),
+        resyncing_(initial_offset > 0) {}
+
+  // Streaming: `src` is positioned at file offset 0 and must outlive the
+  // reader; each refill reads window_blocks * kBlockSize bytes.
+  LogReader(LogSource* src, Reporter* reporter, bool checksum, uint64_t initial_offset, uint32_t flags = 0,
+            size_t window_blocks = 16)
+      : file_(nullptr),
+        file_len_(0),
+        src_(src),
+        window_blocks_(window_blocks ? window_blocks : 1),
         reporter_(reporter),
         checksum_(checksum),
         flags_(flags),
@@ -58,7 +96,7 @@ class LogReader {
     scratch->clear();
     *data = "";
     *size = 0;
-    if (status_ != NVL_CRC32C_OK) return false;
+    if (status_ != NVL_CRC32C_OK || skip_failed_) return false;
     bool in_fragmented_record = false;
     uint64_t prospective_record_offset = 0;
     const char* frag = "";
@@ -155,7 +193,8 @@ class LogReader {
   static const uint64_t kBlock = NVL_LOG_BLOCK_SIZE;
   static const uint64_t kHeader = NVL_LOG_HEADER_SIZE;
 
-  // SkipToInitialBlock (log_reader.cc:36-60), then the one batch scan.
+  // SkipToInitialBlock (log_reader.cc:36-60), then the one batch scan (or,
+  // streaming, the first window).
   void Scan() {
     scanned_ = true;
     uint64_t in_block = initial_offset_ % kBlock;
@@ -163,6 +202,19 @@ class LogReader {
     if (in_block > kBlock - 6) block_start += kBlock;  // don't search a block if we'd be in the trailer
     pos_ = block_start;
     next_ = 0;
+    if (src_) {
+      win_start_ = block_start;
+      if (block_start > 0) {
+        std::string err;
+        if (!src_->Skip(block_start, &err)) {  // ReportDrop(block_start_location, skip_status), unsigned as there
+          if (reporter_ != nullptr && pos_ - block_start >= initial_offset_) reporter_->Drop((size_t)block_start, err.c_str());
+          skip_failed_ = true;
+          return;
+        }
+      }
+      NextWindow();
+      return;
+    }
     if (block_start >= file_len_) {  // skipped to (or past) the end: the first read finds nothing
       nvl_log_event eof = {block_start, block_start, 0u, 0u, NVL_LOG_EOF, 0u};
       events_.assign(1, eof);
@@ -176,9 +228,70 @@ class LogReader {
     events_.resize(status_ == NVL_CRC32C_OK ? ne : 0);
   }
 
+  // Streaming: read the next window and scan it.  A full window is not the
+  // end of the file (the reference's eof_ stays false after a full piece),
+  // so its scan's closing EOF event is dropped and the next refill decides;
+  // a short window ends the file.  A failed read: the whole pieces read
+  // before it are scanned, then the drop of the failing piece is reported
+  // and the reader is at its end (log_reader.cc:205-211).
+  void NextWindow() {
+    events_.clear();
+    next_ = 0;
+    if (src_eof_) {
+      nvl_log_event eof = {win_start_, win_start_, 0u, 0u, NVL_LOG_EOF, 0u};
+      events_.assign(1, eof);
+      return;
+    }
+    const size_t want = (size_t)(window_blocks_ * kBlock);
+    win_.resize(want);
+    std::string err;
+    const size_t got = src_->Read(want, &win_[0], &err);
+    const bool failed = !err.empty();
+    const uint64_t start = win_start_;
+    // pieces the reference would parse: every whole one; the last, short one
+    // too unless the read failed inside it
+    const uint64_t parse = failed ? (uint64_t)got / kBlock * kBlock : (uint64_t)got;
+    if (parse > 0) {
+      const size_t cap = (size_t)(parse / kHeader + parse / kBlock + 4);
+      events_.resize(cap);
+      size_t ne = 0;
+      status_ = nvl_log_scan(win_.data(), parse, start, checksum_ ? 1 : 0, events_.data(), cap, &ne, flags_);
+      events_.resize(status_ == NVL_CRC32C_OK ? ne : 0);
+      if (status_ != NVL_CRC32C_OK) return;
+      if (!events_.empty() && events_.back().kind == NVL_LOG_EOF) events_.pop_back();
+    }
+    win_start_ = start + parse;
+    win_parsed_ = parse;
+    if (failed) {
+      fail_end_ = start + got;  // end_of_buffer_offset_ after the failing Read
+      fail_msg_ = err;
+      src_eof_ = true;
+      has_fail_ = true;
+    } else if (got < want) {
+      src_eof_ = true;
+      // a short window: its scan's EOF (a truncated record at the end of
+      // the file is not a corruption) ends the stream
+      nvl_log_event eof = {start + got, start + got, 0u, 0u, NVL_LOG_EOF, 0u};
+      events_.push_back(eof);
+    }
+  }
+
   // ReadPhysicalRecord (log_reader.cc:199-281) replayed from the scan.
   // pos_ mirrors end_of_buffer_offset_ - buffer_.size().
   unsigned ReadPhysicalRecord(const char** frag, size_t* frag_n) {
+    while (src_ && next_ >= events_.size()) {
+      if (status_ != NVL_CRC32C_OK) return kEof;
+      if (has_fail_) {  // the failing piece: ReportDrop(kBlockSize, status), then the end
+        has_fail_ = false;
+        pos_ = fail_end_;
+        if (reporter_ != nullptr && pos_ - kBlock >= initial_offset_) reporter_->Drop((size_t)kBlock, fail_msg_.c_str());
+        nvl_log_event eof = {fail_end_, fail_end_, 0u, 0u, NVL_LOG_EOF, 0u};
+        events_.assign(1, eof);
+        next_ = 0;
+        break;
+      }
+      NextWindow();
+    }
     if (next_ >= events_.size()) return kEof;
     const nvl_log_event& e = events_[next_];
     switch (e.kind) {
@@ -190,7 +303,7 @@ class LogReader {
           *frag_n = 0;
           return kBadRecord;
         }
-        *frag = file_ + e.offset + kHeader;
+        *frag = (src_ ? win_.data() + (e.offset - (win_start_ - win_parsed())) : file_ + e.offset) + kHeader;
         *frag_n = e.length;
         return e.type;
       case NVL_LOG_BAD_LENGTH:
@@ -218,8 +331,13 @@ class LogReader {
     if (reporter_ != nullptr && pos_ - bytes >= initial_offset_) reporter_->Corruption((size_t)bytes, reason);
   }
 
+  // bytes of win_ that the current events were scanned from
+  uint64_t win_parsed() const { return win_parsed_; }
+
   const char* const file_;
   const uint64_t file_len_;
+  LogSource* const src_;
+  const size_t window_blocks_;
   Reporter* const reporter_;
   const bool checksum_;
   const uint32_t flags_;
@@ -231,6 +349,13 @@ class LogReader {
   size_t next_ = 0;
   uint64_t pos_ = 0;
   uint64_t last_record_offset_ = 0;
+  // streaming state
+  std::string win_;
+  uint64_t win_start_ = 0;   // file offset just past the window parsed last
+  uint64_t win_parsed_ = 0;  // bytes of it parsed
+  bool src_eof_ = false, has_fail_ = false, skip_failed_ = false;
+  uint64_t fail_end_ = 0;
+  std::string fail_msg_;
 };
 
 // ---------------------------------------------------------------------------

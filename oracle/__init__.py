@@ -256,6 +256,8 @@ class _RefFraming:
         lib.ref_log_write.argtypes = [vp, vp, sz, u64, vp, sz, vp]
         lib.ref_log_read.restype = ctypes.c_int
         lib.ref_log_read.argtypes = [vp, sz, ctypes.c_int, u64, vp, sz, vp]
+        lib.ref_log_read_failing.restype = ctypes.c_int
+        lib.ref_log_read_failing.argtypes = [vp, sz, ctypes.c_int, u64, u64, vp, sz, vp]
         lib.ref_read_block.restype = ctypes.c_int
         lib.ref_read_block.argtypes = [vp, sz, u64, u64, ctypes.c_char_p, sz]
         lib.ref_table_scan.restype = ctypes.c_int
@@ -279,6 +281,16 @@ class _RefFraming:
         n = ctypes.c_size_t(0)
         rc = self.lib.ref_log_read(image or b"\0", len(image), int(checksum), initial_offset, out, cap,
                                    ctypes.byref(n))
+        assert rc == 0, rc
+        return out.raw[:n.value].decode()
+
+    def log_read_failing(self, image: bytes, checksum: bool, initial_offset: int, fail_at: int) -> str:
+        """log::Reader over a SequentialFile whose read covering byte fail_at fails."""
+        cap = 64 * (len(image) // 7 + 16) + 4096
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        rc = self.lib.ref_log_read_failing(image or b"\0", len(image), int(checksum), initial_offset, fail_at, out,
+                                           cap, ctypes.byref(n))
         assert rc == 0, rc
         return out.raw[:n.value].decode()
 

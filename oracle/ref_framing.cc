@@ -65,6 +65,41 @@ class StringSource : public leveldb::SequentialFile {
   leveldb::Slice contents_;
 };
 
+// StringSource whose read covering byte `fail_at` fails: it returns the bytes
+// before fail_at and IOError (a disk error in the middle of a WAL).
+class FailingSource : public leveldb::SequentialFile {
+ public:
+  FailingSource(const char* d, size_t n, uint64_t fail_at) : d_(d), n_(n), fail_at_(fail_at) {}
+  leveldb::Status Read(size_t n, leveldb::Slice* result, char* scratch) override {
+    if (n > n_ - pos_) n = n_ - pos_;
+    if (fail_at_ >= pos_ && fail_at_ < pos_ + n) {
+      const size_t m = (size_t)(fail_at_ - pos_);
+      memcpy(scratch, d_ + pos_, m);
+      *result = leveldb::Slice(scratch, m);
+      pos_ += m;
+      return leveldb::Status::IOError("injected read failure");
+    }
+    memcpy(scratch, d_ + pos_, n);
+    *result = leveldb::Slice(scratch, n);
+    pos_ += n;
+    return leveldb::Status::OK();
+  }
+  leveldb::Status Skip(uint64_t n) override {
+    if (n > n_ - pos_) {
+      pos_ = n_;
+      return leveldb::Status::NotFound("in-memory file skipped past end");
+    }
+    pos_ += n;
+    return leveldb::Status::OK();
+  }
+
+ private:
+  const char* d_;
+  size_t n_;
+  uint64_t fail_at_;
+  size_t pos_ = 0;
+};
+
 class MemRandomAccess : public leveldb::RandomAccessFile {
  public:
   MemRandomAccess(const char* d, size_t n) : d_(d), n_(n) {}
@@ -130,6 +165,27 @@ __attribute__((visibility("default")))
 int ref_log_read(const uint8_t* file, size_t len, int checksum, uint64_t initial_offset, char* trace, size_t cap,
                  size_t* trace_len) {
   StringSource src(reinterpret_cast<const char*>(file), len);
+  std::string t;
+  TraceReporter rep;
+  rep.trace = &t;
+  leveldb::log::Reader r(&src, &rep, checksum != 0, initial_offset);
+  leveldb::Slice rec;
+  std::string scratch;
+  while (r.ReadRecord(&rec, &scratch)) {
+    char buf[96];
+    snprintf(buf, sizeof(buf), "R %llu %zu %u\n", (unsigned long long)r.LastRecordOffset(), rec.size(),
+             leveldb::crc32c::Value(rec.data(), rec.size()));
+    t.append(buf);
+  }
+  t.append("E\n");
+  return copy_out(t, trace, cap, trace_len);
+}
+
+// The same over a FailingSource (fail_at >= len: no failure).
+__attribute__((visibility("default")))
+int ref_log_read_failing(const uint8_t* file, size_t len, int checksum, uint64_t initial_offset, uint64_t fail_at,
+                         char* trace, size_t cap, size_t* trace_len) {
+  FailingSource src(reinterpret_cast<const char*>(file), len, fail_at);
   std::string t;
   TraceReporter rep;
   rep.trace = &t;

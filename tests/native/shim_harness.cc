@@ -22,6 +22,46 @@ struct TraceReporter : nvl::shims::LogReader::Reporter {
     trace->append(reason);
     trace->push_back('\n');
   }
+  void Drop(size_t bytes, const char* status) override {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "C %zu ", bytes);
+    trace->append(buf);
+    trace->append(status);
+    trace->push_back('\n');
+  }
+};
+
+// A LogSource over memory whose read covering byte fail_at fails (the bytes
+// before it are returned), as oracle/ref_framing.cc's FailingSource.
+struct MemSource : nvl::shims::LogSource {
+  const char* d;
+  size_t n;
+  uint64_t fail_at;
+  size_t pos = 0;
+  size_t reads = 0;
+  size_t Read(size_t want, char* buf, std::string* error) override {
+    ++reads;
+    if (want > n - pos) want = n - pos;
+    if (fail_at >= pos && fail_at < pos + want) {
+      const size_t m = (size_t)(fail_at - pos);
+      memcpy(buf, d + pos, m);
+      pos += m;
+      *error = "IO error: injected read failure";
+      return m;
+    }
+    memcpy(buf, d + pos, want);
+    pos += want;
+    return want;
+  }
+  bool Skip(uint64_t k, std::string* error) override {
+    if (k > n - pos) {
+      pos = n;
+      *error = "NotFound: in-memory file skipped past end";
+      return false;
+    }
+    pos += k;
+    return true;
+  }
 };
 
 int copy_out(const std::string& s, void* out, size_t cap, size_t* out_len) {
@@ -71,6 +111,35 @@ int shim_log_read(const uint8_t* file, size_t len, int checksum, uint64_t initia
   }
   if (r.status() != NVL_CRC32C_OK) return r.status();
   t.append("E\n");
+  return copy_out(t, trace, cap, trace_len);
+}
+
+// The streaming LogReader over a MemSource read window_blocks pieces at a
+// time; same trace, plus the number of source reads in *reads.
+__attribute__((visibility("default")))
+int shim_log_read_stream(const uint8_t* file, size_t len, int checksum, uint64_t initial_offset, uint32_t flags,
+                         size_t window_blocks, uint64_t fail_at, char* trace, size_t cap, size_t* trace_len,
+                         size_t* reads) {
+  std::string t;
+  TraceReporter rep;
+  rep.trace = &t;
+  MemSource src;
+  src.d = reinterpret_cast<const char*>(file);
+  src.n = len;
+  src.fail_at = fail_at;
+  nvl::shims::LogReader r(&src, &rep, checksum != 0, initial_offset, flags, window_blocks);
+  const char* d;
+  size_t n;
+  std::string scratch;
+  while (r.ReadRecord(&d, &n, &scratch)) {
+    char buf[96];
+    snprintf(buf, sizeof(buf), "R %llu %zu %u\n", (unsigned long long)r.LastRecordOffset(), n,
+             nvl_crc32c_value(d, n));
+    t.append(buf);
+  }
+  if (r.status() != NVL_CRC32C_OK) return r.status();
+  t.append("E\n");
+  *reads = src.reads;
   return copy_out(t, trace, cap, trace_len);
 }
 

@@ -43,6 +43,8 @@ def shim():
     lib.shim_log_write.argtypes = [vp, vp, sz, u64, u32, vp, sz, vp]
     lib.shim_log_read.restype = ctypes.c_int
     lib.shim_log_read.argtypes = [vp, sz, ctypes.c_int, u64, u32, vp, sz, vp]
+    lib.shim_log_read_stream.restype = ctypes.c_int
+    lib.shim_log_read_stream.argtypes = [vp, sz, ctypes.c_int, u64, u32, sz, u64, vp, sz, vp, vp]
     return lib
 
 
@@ -79,6 +81,24 @@ def _reader(shim, flags):
     return r
 
 
+NO_FAIL = (1 << 64) - 1
+
+
+def _stream_reader(shim, flags, window_blocks, fail_at=NO_FAIL):
+    """The streaming shims::LogReader (a LogSource read window_blocks pieces at a
+    time); returns (trace, number of source reads)."""
+    def r(image, checksum, initial_offset):
+        cap = 64 * (len(image) // 7 + 16) + 4096
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        reads = ctypes.c_size_t(0)
+        rc = shim.shim_log_read_stream(image or b"\0", len(image), int(checksum), initial_offset, flags,
+                                       window_blocks, fail_at, out, cap, ctypes.byref(n), ctypes.byref(reads))
+        assert rc == 0, rc
+        return out.raw[:n.value].decode(), reads.value
+    return r
+
+
 def _check_log_fixtures(shim, port, flags):
     cases = load_golden("log_cases")["cases"]
     assert len(cases) >= 300
@@ -104,6 +124,74 @@ def test_log_fixtures_gpu(shim, port):
     if not gpu_present():
         pytest.skip("no GPU")
     _check_log_fixtures(shim, port, 0)
+
+
+def _check_log_fixtures_streamed(shim, port, flags, windows):
+    """The 334 log fixtures through the streaming reader, fed in windows of
+    1, 3 and 17 blocks: the same trace as the whole-image reader (and as the
+    reference, which the fixture traces come from), with ceil(len / window)
+    + 1 reads at most (db/log_reader.cc:199-218 reads kBlockSize at a time)."""
+    cases = load_golden("log_cases")["cases"]
+    w = _writer(shim, flags)
+    for wb in windows:
+        r = _stream_reader(shim, flags, wb)
+        for c in cases:
+            bad = fc.mutate(port, fc.write_image(port, c, w), c["mutations"])
+            trace, reads = r(bad, c["checksum"], c["initial_offset"])
+            if "trace" in c:
+                assert trace == c["trace"], (wb, c["name"])
+            else:
+                assert (port.value(trace.encode()), trace.count("\n")) == (c["trace_crc"], c["trace_lines"]), \
+                    (wb, c["name"])
+            assert reads <= len(bad) // (wb * 32768) + 2, (wb, c["name"], reads)
+
+
+def test_log_fixtures_streamed_host(shim, port):
+    _check_log_fixtures_streamed(shim, port, HOST, (1, 3, 17))
+
+
+@pytest.mark.gpu
+def test_log_fixtures_streamed_gpu(shim, port):
+    if not gpu_present():
+        pytest.skip("no GPU")
+    _check_log_fixtures_streamed(shim, port, 0, (1, 3, 17))
+
+
+def test_log_stream_read_errors_vs_reference_live(shim, port):
+    """A read that fails part way (IOError with the bytes before the failure):
+    the streaming reader reports the reference's ReportDrop(kBlockSize,
+    status) (db/log_reader.cc:205-211) -- same trace as the reference's
+    log::Reader over the same failing SequentialFile, for failures at block
+    boundaries, inside blocks, before/after initial_offset, and in windows of
+    1, 3 and 17 blocks; a skip past the end (initial_offset beyond the file)
+    too."""
+    import oracle
+    if not oracle.ref_framing_available():
+        pytest.skip("reference framing harness not built")
+    rf = oracle.ref_framing()
+    w = _writer(shim, HOST)
+    rng = np.random.default_rng(2024)
+    specs = fc.random_cases(40, seed=4242)
+    n = 0
+    for spec in specs:
+        img = fc.write_image(port, spec, w)
+        muts, io = fc.resolve(port, spec, img)
+        bad = fc.mutate(port, img, muts)
+        L = len(bad)
+        fails = {NO_FAIL, 0, L // 2, max(0, L - 1)}
+        for k in range(1, L // 32768 + 1):
+            fails |= {32768 * k, 32768 * k - 1, 32768 * k + 7}
+        fails |= {int(x) for x in rng.integers(0, L + 1, 3)}
+        for fa in sorted(fails):
+            want = rf.log_read_failing(bad, spec["checksum"], io, min(fa, (1 << 64) - 1))
+            for wb in (1, 3, 17):
+                got, _ = _stream_reader(shim, HOST, wb, fa)(bad, spec["checksum"], io)
+                assert got == want, (spec["name"], fa, wb)
+                n += 1
+        far = L + 5 * 32768  # initial_offset past the end: Skip fails (never reported), no records
+        got, _ = _stream_reader(shim, HOST, 3)(bad, spec["checksum"], far)
+        assert got == rf.log_read_failing(bad, spec["checksum"], far, NO_FAIL), spec["name"]
+    assert n > 500
 
 
 def test_log_vs_reference_live(shim, port):

@@ -322,5 +322,52 @@ def ref_framing() -> _RefFraming:
     return _ref_framing
 
 
+class _RefTable:
+    """ctypes view of ``oracle/_ref/libref_table.so`` (oracle/ref_table.cc): the
+    reference's own TableBuilder, writing to memory or through shims::TableFile."""
+
+    def __init__(self) -> None:
+        self.path = os.path.join(HERE, "_ref", "libref_table.so")
+        lib = ctypes.CDLL(self.path, mode=os.RTLD_LOCAL)
+        vp, sz, u64, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32
+        lib.ref_table_build.restype = ctypes.c_int
+        lib.ref_table_build.argtypes = [vp, vp, vp, sz, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, vp, sz,
+                                        vp, vp, sz, vp]
+        self.lib = lib
+
+    def build(self, keys, values, block_size=4096, restart_interval=16, bloom_bits=0, via_shim=False,
+              seal_flags=0):
+        """(image bytes, block handles [(offset, size)] -- via_shim only)."""
+        kv = b"".join(k + v for k, v in zip(keys, values)) or b"\0"
+        kl = np.array([len(k) for k in keys] or [0], dtype=np.uint64)
+        vl = np.array([len(v) for v in values] or [0], dtype=np.uint64)
+        cap = len(kv) * 2 + 64 * len(keys) + (1 << 16)
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t(0)
+        hcap = 2 * (len(kv) // 16 + 64)
+        hd = np.zeros(hcap, dtype=np.uint64)
+        nh = ctypes.c_size_t(0)
+        rc = self.lib.ref_table_build(kv, kl.ctypes.data, vl.ctypes.data, len(keys), block_size, restart_interval,
+                                      bloom_bits, int(via_shim), seal_flags, out, cap, ctypes.byref(n),
+                                      hd.ctypes.data, hcap, ctypes.byref(nh))
+        assert rc == 0, rc
+        hs = [(int(hd[2 * k]), int(hd[2 * k + 1])) for k in range(nh.value)]
+        return out.raw[:n.value], hs
+
+
+_ref_table = None
+
+
+def ref_table():
+    global _ref_table
+    if _ref_table is None:
+        _ref_table = _RefTable()
+    return _ref_table
+
+
+def ref_table_available() -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libref_table.so"))
+
+
 def ref_framing_available() -> bool:
     return os.path.exists(os.path.join(HERE, "_ref", "libref_framing.so"))

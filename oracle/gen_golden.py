@@ -114,7 +114,8 @@ def sweep() -> dict:
 def framing() -> dict:
     """SSTable block trailers (table/table_builder.cc:183-188, checked by
     table/format.cc:90-96) and log record headers (db/log_writer.cc:88-97,
-    checked by db/log_reader.cc:253-256) for synthetic contents."""
+    checked by db/log_reader.cc:253-256) for synthetic contents, plus whole
+    tables written by the reference's own TableBuilder."""
     p = oracle.port()
     rng = np.random.default_rng(99)
     blocks = []
@@ -135,7 +136,31 @@ def framing() -> dict:
         crc = both(lambda r: r.extend(type_crc, payload))
         records.append({"len": n, "seed": 0x5EED00C0 + i, "type": rtype, "type_crc": type_crc,
                         "crc": crc, "masked": both(lambda r: r.mask(crc))})
-    return {"sstable_blocks": blocks, "log_records": records}
+    # Real tables: the reference's TableBuilder (oracle/ref_table.cc) over
+    # deterministic key/value sets; every block (data, filter, metaindex,
+    # index) with its handle, and the real data blocks appended to
+    # sstable_blocks as well.
+    tables = []
+    if oracle.ref_table_available():
+        rt = oracle.ref_table()
+        for ti, (n, bs, ri, bloom) in enumerate([(300, 1024, 16, 0), (400, 4096, 4, 10), (1, 4096, 16, 0),
+                                                 (120, 256, 1, 10)]):
+            keys = [b"key%08d" % (i * 7 + ti) for i in range(n)]
+            vals = [p.fill(0x7AB1E000 + ti * 1000 + i, 0, int(rng.integers(0, 300))).tobytes() for i in range(n)]
+            img, _ = rt.build(keys, vals, bs, ri, bloom)
+            img2, hs = rt.build(keys, vals, bs, ri, bloom, via_shim=True, seal_flags=0x100)
+            assert img2 == img, "TableFile seal differs from the reference TableBuilder"
+            tables.append({"entries": n, "block_size": bs, "restart_interval": ri, "bloom_bits": bloom,
+                           "hex": img.hex(), "handles": hs, "image_crc": both(lambda r: r.value(img))})
+            if ti == 1:
+                for (o, sz) in hs:
+                    data = img[o:o + sz]
+                    btype = img[o + sz]
+                    crc = both(lambda r: r.extend(r.value(data), bytes([btype])))
+                    blocks.append({"hex": data.hex(), "type": btype, "crc": crc, "masked": both(lambda r: r.mask(crc)),
+                                   "check": both(lambda r: r.value(data + bytes([btype]))),
+                                   "source": "TableBuilder (oracle/ref_table.cc), table 1"})
+    return {"sstable_blocks": blocks, "log_records": records, "sstable_tables": tables}
 
 
 def log_cases() -> dict:
@@ -268,7 +293,8 @@ def main() -> None:
     os.makedirs(GOLDEN, exist_ok=True)
     provenance = {"generator": "oracle/gen_golden.py",
                   "reference_builds": [oracle.ref("sse").path, oracle.ref("table").path,
-                                       os.path.join(os.path.dirname(oracle.ref("sse").path), "libref_framing.so")]}
+                                       os.path.join(os.path.dirname(oracle.ref("sse").path), "libref_framing.so"),
+                                       os.path.join(os.path.dirname(oracle.ref("sse").path), "libref_table.so")]}
     for name, fn in [("kat", kat), ("sweep", sweep), ("framing", framing), ("log_cases", log_cases),
                      ("table_cases", table_cases)]:
         if only and name not in only:

@@ -116,6 +116,15 @@ typedef struct nvl_table_block {
 NVL_API int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
                                      size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags);
 
+/* The same for a table image already in device memory (HBM) on `stream`'s
+ * device (a hipStream_t; NULL = the null stream): the footer, index and
+ * metaindex blocks come back in small copies and are parsed on the host,
+ * every other block is checked in place by one batch and a trailer-check
+ * kernel, and only the verdicts return.  Same results as
+ * nvl_sstable_verify_table on the same bytes; synchronous on `stream`. */
+NVL_API int nvl_sstable_verify_table_dev(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
+                                         size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, void* stream);
+
 /* ---- log files ----------------------------------------------------------- */
 
 #define NVL_LOG_BLOCK_SIZE 32768 /* db/log_format.h:27 */

@@ -59,6 +59,7 @@ SIGNATURES = {
     "nvl_log_scan": (_int, [_vp, _u64, _u64, _int, _vp, _sz, _vp, _u32]),
     "nvl_log_seal": (_int, [_vp, _u64, _vp, _sz, _u32]),
     "nvl_sstable_verify_table": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _vp, _u32]),
+    "nvl_sstable_verify_table_dev": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _vp, _vp]),
 }
 
 FRAMING_HOST = 0x100

@@ -10,6 +10,7 @@
 
 #include <vector>
 
+#include "crc32c_framing_core.h"
 #include "crc32c_internal.h"
 #include "crc32c_math.h"
 #include "nvl_framing.h"
@@ -40,11 +41,6 @@ int value_many(const uint8_t* region, uint64_t region_len, const std::vector<uin
     return NVL_CRC32C_OK;
   }
   return nvl_crc32c_batch_region_host(region, region_len, off.data(), len.data(), nullptr, 0, crc->data(), n, 0);
-}
-
-bool block_in_file(const nvl_block_handle& h, uint64_t file_len) {
-  return h.size <= file_len && h.offset <= file_len - h.size &&
-         file_len - h.size - h.offset >= (uint64_t)NVL_BLOCK_TRAILER_SIZE;
 }
 
 constexpr uint64_t kLogBlock = NVL_LOG_BLOCK_SIZE;
@@ -309,20 +305,50 @@ int nvl_log_seal(void* data, uint64_t len, const uint64_t* header_offsets, size_
   return NVL_CRC32C_OK;
 }
 
-int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
-                             size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags) {
-  if (n_blocks) *n_blocks = 0;
-  if (n_bad) *n_bad = 0;
-  if ((!file && file_len) || !n_blocks || !table_status) return NVL_CRC32C_EINVAL;
-  const uint8_t* f = static_cast<const uint8_t*>(file);
-  *table_status = NVL_TABLE_OK;
+}  // extern "C"
 
-  // Table::Open (table/table.cc:38-55): footer.
-  if (file_len < NVL_FOOTER_SIZE) {
+namespace nvl {
+namespace {
+
+struct HostTable : TableSource {
+  const uint8_t* f;
+  uint64_t len;
+  uint32_t flags;
+  int read(uint64_t off, uint64_t n, uint8_t* dst) override {
+    memcpy(dst, f + off, n);
+    return NVL_CRC32C_OK;
+  }
+  int verify(const std::vector<nvl_block_handle>& h, std::vector<uint8_t>* verdict) override {
+    verdict->assign(h.size(), NVL_BLOCK_OK);
+    if (h.empty()) return NVL_CRC32C_OK;
+    return nvl_sstable_verify_blocks(f, len, h.data(), h.size(), verdict->data(), nullptr, flags);
+  }
+};
+
+// ReadBlock's trailer checks on one block held on the host with its trailer.
+uint8_t host_block_verdict(const std::vector<uint8_t>& b, uint64_t size) {
+  const uint32_t crc = host_extend(0, b.data(), size + 1);
+  if (crc != unmask(load_le32(b.data() + size + 1))) return NVL_BLOCK_CHECKSUM_MISMATCH;
+  if (b[size] != 0 && b[size] != 1) return NVL_BLOCK_BAD_TYPE;
+  return NVL_BLOCK_OK;
+}
+
+}  // namespace
+
+// Table::Open (table/table.cc:38-82), then ReadBlock with verify_checksums of
+// every block the index and metaindex point at.  The index and metaindex
+// blocks are small: read to the host and checked there; every other block's
+// check goes to the source's batch.
+int verify_table_core(TableSource& src, uint64_t file_len, nvl_table_block* blocks, size_t cap, size_t* n_blocks,
+                      uint32_t* table_status, uint64_t* n_bad) {
+  *table_status = NVL_TABLE_OK;
+  if (file_len < NVL_FOOTER_SIZE) {  // table.cc:44-46
     *table_status = NVL_TABLE_TOO_SHORT;
     return NVL_CRC32C_OK;
   }
-  const uint8_t* footer = f + file_len - NVL_FOOTER_SIZE;
+  uint8_t footer[NVL_FOOTER_SIZE];
+  int rc = src.read(file_len - NVL_FOOTER_SIZE, NVL_FOOTER_SIZE, footer);
+  if (rc != NVL_CRC32C_OK) return rc;
   const uint64_t magic = (uint64_t)load_le32(footer + 40) | ((uint64_t)load_le32(footer + 44) << 32);
   if (magic != kTableMagic) {  // format.cc:43-51
     *table_status = NVL_TABLE_BAD_MAGIC;
@@ -334,66 +360,57 @@ int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_bloc
     *table_status = NVL_TABLE_BAD_FOOTER;
     return NVL_CRC32C_OK;
   }
-
-  // Speculative parse of the index and metaindex blocks (their CRCs are
-  // checked in the same batch as the blocks they point at).
-  auto contents = [&](const nvl_block_handle& h) { return block_in_file(h, file_len) ? f + h.offset : nullptr; };
+  // the two structure blocks with their trailers (verdict: truncated when
+  // they do not fit the file, format.cc:82-85)
+  std::vector<uint8_t> index_b, meta_b;
+  uint8_t v_index = NVL_BLOCK_TRUNCATED, v_meta = NVL_BLOCK_TRUNCATED;
+  if (block_in_file(index_h, file_len)) {
+    index_b.resize(index_h.size + NVL_BLOCK_TRAILER_SIZE);
+    if ((rc = src.read(index_h.offset, index_b.size(), index_b.data())) != NVL_CRC32C_OK) return rc;
+    v_index = host_block_verdict(index_b, index_h.size);
+  }
+  if (block_in_file(meta_h, file_len)) {
+    meta_b.resize(meta_h.size + NVL_BLOCK_TRAILER_SIZE);
+    if ((rc = src.read(meta_h.offset, meta_b.size(), meta_b.data())) != NVL_CRC32C_OK) return rc;
+    v_meta = host_block_verdict(meta_b, meta_h.size);
+  }
   std::vector<nvl_block_handle> data_h, meta_blocks;
   std::vector<uint8_t> data_bad, meta_bad;
   uint32_t index_parse = NVL_TABLE_OK;
-  const uint8_t* index_data = contents(index_h);
-  if (index_data && index_data[index_h.size] == 0)
-    index_parse = block_handles(index_data, index_h.size, &data_h, &data_bad);
-  const uint8_t* meta_data = contents(meta_h);
-  if (meta_data && meta_data[meta_h.size] == 0) block_handles(meta_data, meta_h.size, &meta_blocks, &meta_bad);
-
-  if (!blocks) {
-    // Size query: the list's length depends only on the index and metaindex
-    // verdicts, so only those two blocks are checked (host CRC) -- no batch.
-    const nvl_block_handle two[2] = {index_h, meta_h};
-    uint8_t v2[2];
-    const int rq = nvl_sstable_verify_blocks(f, file_len, two, 2, v2, nullptr, flags | NVL_FRAMING_HOST);
-    if (rq != NVL_CRC32C_OK) return rq;
-    size_t cnt = 1;
-    if (v2[0] != NVL_BLOCK_OK) {
-      *table_status = NVL_TABLE_INDEX_UNREADABLE;
-    } else if (index_data[index_h.size] != 0) {
-      *table_status = NVL_TABLE_COMPRESSED_INDEX;
-    } else {
-      const bool meta_ok = v2[1] == NVL_BLOCK_OK && meta_data[meta_h.size] == 0;
-      cnt += 1 + (meta_ok ? meta_blocks.size() : 0) + data_h.size();
-      *table_status = index_parse;
-    }
-    *n_blocks = cnt;
-    return NVL_CRC32C_OK;
-  }
-
-  // One CRC batch: index, metaindex, then every decodable in-file handle.
-  std::vector<nvl_block_handle> all;
-  all.reserve(2 + meta_blocks.size() + data_h.size());
-  all.push_back(index_h);
-  all.push_back(meta_h);
-  for (size_t i = 0; i < meta_blocks.size(); ++i) all.push_back(meta_blocks[i]);
-  for (size_t i = 0; i < data_h.size(); ++i) all.push_back(data_h[i]);
-  std::vector<uint8_t> verdict(all.size());
-  const int rc = nvl_sstable_verify_blocks(f, file_len, all.data(), all.size(), verdict.data(), nullptr, flags);
-  if (rc != NVL_CRC32C_OK) return rc;
+  if (v_index == NVL_BLOCK_OK && index_b[index_h.size] == 0)
+    index_parse = block_handles(index_b.data(), index_h.size, &data_h, &data_bad);
+  const bool meta_ok = v_meta == NVL_BLOCK_OK && meta_b[meta_h.size] == 0;
+  if (meta_ok) block_handles(meta_b.data(), meta_h.size, &meta_blocks, &meta_bad);
 
   std::vector<nvl_table_block> out;
   auto emit = [&](const nvl_block_handle& h, uint32_t role, uint32_t v) {
     out.push_back(nvl_table_block{h.offset, h.size, role, v});
   };
-  emit(index_h, NVL_TBLOCK_INDEX, verdict[0]);
-  if (verdict[0] != NVL_BLOCK_OK) {  // Table::Open fails on the index block (table.cc:58-66)
+  if (v_index != NVL_BLOCK_OK) {  // Table::Open fails on the index block (table.cc:58-66)
+    emit(index_h, NVL_TBLOCK_INDEX, v_index);
     *table_status = NVL_TABLE_INDEX_UNREADABLE;
-  } else if (index_data[index_h.size] != 0) {
+  } else if (index_b[index_h.size] != 0) {
+    emit(index_h, NVL_TBLOCK_INDEX, v_index);
     *table_status = NVL_TABLE_COMPRESSED_INDEX;
   } else {
-    emit(meta_h, NVL_TBLOCK_METAINDEX, verdict[1]);
-    const bool meta_ok = verdict[1] == NVL_BLOCK_OK && meta_data[meta_h.size] == 0;
-    size_t k = 2;
+    const size_t cnt = 2 + meta_blocks.size() + data_h.size();
+    if (!blocks) {  // size query: the list's length needs no batch
+      *n_blocks = cnt;
+      *table_status = index_parse;
+      return NVL_CRC32C_OK;
+    }
+    // one batch: every meta and data block
+    std::vector<nvl_block_handle> all;
+    all.reserve(meta_blocks.size() + data_h.size());
+    for (size_t i = 0; i < meta_blocks.size(); ++i) all.push_back(meta_blocks[i]);
+    for (size_t i = 0; i < data_h.size(); ++i) all.push_back(data_h[i]);
+    std::vector<uint8_t> verdict;
+    if ((rc = src.verify(all, &verdict)) != NVL_CRC32C_OK) return rc;
+    emit(index_h, NVL_TBLOCK_INDEX, v_index);
+    emit(meta_h, NVL_TBLOCK_METAINDEX, v_meta);
+    size_t k = 0;
     for (size_t i = 0; i < meta_blocks.size(); ++i, ++k)
-      if (meta_ok) emit(meta_blocks[i], NVL_TBLOCK_META, meta_bad[i] ? NVL_BLOCK_BAD_HANDLE : verdict[k]);
+      emit(meta_blocks[i], NVL_TBLOCK_META, meta_bad[i] ? NVL_BLOCK_BAD_HANDLE : verdict[k]);
     for (size_t i = 0; i < data_h.size(); ++i, ++k)
       emit(data_h[i], NVL_TBLOCK_DATA, data_bad[i] ? NVL_BLOCK_BAD_HANDLE : verdict[k]);
     *table_status = index_parse;
@@ -404,9 +421,27 @@ int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_bloc
     for (const nvl_table_block& t : out) b += t.verdict != NVL_BLOCK_OK;
     *n_bad = b;
   }
+  if (!blocks) return NVL_CRC32C_OK;
   if (out.size() > cap) return NVL_CRC32C_ENOSPC;
   if (!out.empty()) memcpy(blocks, out.data(), out.size() * sizeof(nvl_table_block));
   return NVL_CRC32C_OK;
 }
+
+}  // namespace nvl
+
+extern "C" {
+
+int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
+                             size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags) {
+  if (n_blocks) *n_blocks = 0;
+  if (n_bad) *n_bad = 0;
+  if ((!file && file_len) || !n_blocks || !table_status) return NVL_CRC32C_EINVAL;
+  nvl::HostTable src;
+  src.f = static_cast<const uint8_t*>(file);
+  src.len = file_len;
+  src.flags = flags;
+  return nvl::verify_table_core(src, file_len, blocks, cap, n_blocks, table_status, n_bad);
+}
+
 
 }  // extern "C"

@@ -77,6 +77,9 @@ hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);
+// verdict[i] = NVL_BLOCK_* of the trailer at file[off[i] + len1[i] - 1] against crc[i]
+hipError_t launch_trailer_verdicts(const void* file, const uint64_t* off, const uint64_t* len1, const uint32_t* crc,
+                                   uint64_t n, uint8_t* verdict, hipStream_t st);
 
 // Exclusive prefix sum over n u64 (crc32c_scan.hip, hipCUB).
 size_t scan_temp_bytes(uint64_t n);

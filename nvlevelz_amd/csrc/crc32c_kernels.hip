@@ -2193,6 +2193,20 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   NVL_FSTAMP(7);
 }
 
+// ReadBlock's trailer checks (table/format.cc:88-135) for blocks whose CRCs
+// a batch just computed over the device-resident table: len1[i] = size + 1
+// (block | type), the trailer's type byte at off + size, its masked CRC after.
+__global__ void crc32c_trailer_verdicts(const uint8_t* __restrict__ f, const uint64_t* __restrict__ off,
+                                        const uint64_t* __restrict__ len1, const uint32_t* __restrict__ crc,
+                                        uint64_t n, uint8_t* __restrict__ verdict) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* t = f + off[i] + len1[i] - 1u;
+  const uint32_t stored = (uint32_t)t[1] | ((uint32_t)t[2] << 8) | ((uint32_t)t[3] << 16) | ((uint32_t)t[4] << 24);
+  verdict[i] = crc[i] != nvl::unmask(stored) ? 2u /* NVL_BLOCK_CHECKSUM_MISMATCH */
+                                             : (t[0] > 1u ? 3u /* NVL_BLOCK_BAD_TYPE */ : 0u);
+}
+
 // Synthetic stream: one thread per 8-byte word.
 __global__ void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t words_per_block, uint64_t nwords,
                                      uint64_t first_block, uint64_t block_step, uint64_t seed) {
@@ -2211,6 +2225,14 @@ __global__ void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t words_
 
 // ---------------------------------------------------------------------------
 // launchers (host)
+
+hipError_t launch_trailer_verdicts(const void* file, const uint64_t* off, const uint64_t* len1, const uint32_t* crc,
+                                   uint64_t n, uint8_t* verdict, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(dev::crc32c_trailer_verdicts, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const uint8_t*>(file), off, len1, crc, n, verdict);
+  return hipGetLastError();
+}
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st) {

@@ -159,6 +159,30 @@ def verify_table(image: BytesLike, *, host: bool = False) -> TableReport:
     return TableReport(st.value, blocks)
 
 
+def verify_table_dev(image, stream=None) -> TableReport:
+    """verify_table for an SSTable image already in device memory: a 1-D
+    uint8 torch tensor on the GPU (nvl_sstable_verify_table_dev; only the
+    footer, index and metaindex come back to the host)."""
+    import torch
+    if not (isinstance(image, torch.Tensor) and image.is_cuda and image.dtype == torch.uint8 and image.dim() == 1
+            and image.is_contiguous()):
+        raise TypeError("verify_table_dev: a contiguous 1-D uint8 tensor on the GPU")
+    st_ = torch.cuda.current_stream(image.device).cuda_stream if stream is None else stream
+    n = image.numel()
+    cnt = ctypes.c_size_t(0)
+    st = ctypes.c_uint32(0)
+    bad = ctypes.c_uint64(0)
+    with torch.cuda.device(image.device):
+        _check(_lib.lib.nvl_sstable_verify_table_dev(image.data_ptr(), n, None, 0, ctypes.byref(cnt), ctypes.byref(st),
+                                                     ctypes.byref(bad), st_), "verify_table_dev")
+        cap = max(cnt.value, 1)
+        arr = (_lib.TableBlock * cap)()
+        _check(_lib.lib.nvl_sstable_verify_table_dev(image.data_ptr(), n, arr, cap, ctypes.byref(cnt), ctypes.byref(st),
+                                                     ctypes.byref(bad), st_), "verify_table_dev")
+    blocks = [TableBlockReport(a.offset, a.size, ROLE_TEXT[a.role], a.verdict) for a in arr[:cnt.value]]
+    return TableReport(st.value, blocks)
+
+
 LOG_KIND = {_lib.LOG_RECORD: "record", _lib.LOG_BAD_LENGTH: "bad record length",
             _lib.LOG_CHECKSUM: "checksum mismatch", _lib.LOG_ZERO: "zero", _lib.LOG_EOF: "eof"}
 

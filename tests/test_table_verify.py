@@ -67,6 +67,27 @@ def verify(L, img: bytes, flags: int):
     return st.value, blocks
 
 
+def verify_dev(L, img: bytes):
+    """nvl_sstable_verify_table_dev on a device copy of img (size query, then the list)."""
+    import torch
+    d = torch.frombuffer(bytearray(img or b"\0"), dtype=torch.uint8)[:len(img)].cuda()
+    st_ = torch.cuda.current_stream().cuda_stream
+    n = ctypes.c_size_t(0)
+    st = ctypes.c_uint32(0)
+    nb = ctypes.c_uint64(0)
+    lib = L.lib
+    assert lib.nvl_sstable_verify_table_dev(d.data_ptr(), len(img), None, 0, ctypes.byref(n), ctypes.byref(st),
+                                            ctypes.byref(nb), st_) == 0
+    q_n, q_st = n.value, st.value
+    arr = (L.TableBlock * max(n.value, 1))()
+    assert lib.nvl_sstable_verify_table_dev(d.data_ptr(), len(img), arr, n.value, ctypes.byref(n), ctypes.byref(st),
+                                            ctypes.byref(nb), st_) == 0
+    assert (q_n, q_st) == (n.value, st.value)
+    blocks = [(a.offset, a.size, a.role, a.verdict) for a in arr[:n.value]]
+    assert nb.value == sum(b[3] != 0 for b in blocks)
+    return st.value, blocks
+
+
 def via_header(harness, img: bytes, flags: int):
     cap = 64 * (len(img) // 8 + 16)
     out = ctypes.create_string_buffer(cap)
@@ -99,6 +120,28 @@ def test_table_cases_golden_gpu(L, harness, port):
     if not gpu_present():
         pytest.skip("no GPU")
     _check_golden(L, harness, port, 0)
+
+
+@pytest.mark.gpu
+def test_table_cases_golden_device_resident(L, port):
+    """The same 330 reference traces through nvl_sstable_verify_table_dev on
+    device copies of the images (the table already in HBM)."""
+    if not gpu_present():
+        pytest.skip("no GPU")
+    for c in load_golden("table_cases")["cases"]:
+        img, _ = tc.build(port, c)
+        assert verify_dev(L, img) == tc.expected(c["trace"]), c["name"]
+
+
+def test_table_verify_dev_arguments(L):
+    lib = L.lib
+    n = ctypes.c_size_t(7)
+    st = ctypes.c_uint32(9)
+    assert lib.nvl_sstable_verify_table_dev(None, 5, None, 0, ctypes.byref(n), ctypes.byref(st), None, None) == L.EINVAL
+    assert lib.nvl_sstable_verify_table_dev(None, 0, None, 0, None, ctypes.byref(st), None, None) == L.EINVAL
+    # a file too short to be a table needs no device access
+    assert lib.nvl_sstable_verify_table_dev(None, 0, None, 0, ctypes.byref(n), ctypes.byref(st), None, None) == 0
+    assert (n.value, st.value) == (0, L.TABLE_TOO_SHORT)
 
 
 def test_table_cases_vs_reference_live(L, port):
@@ -188,6 +231,8 @@ def test_table_verify_large_gpu(L, port):
     assert st == 0
     assert [i for i, b in enumerate(blocks[2:]) if b[3]] == bad_idx
     assert all(blocks[2 + k][3] == L.BLOCK_CHECKSUM_MISMATCH for k in bad_idx)
+    # the table already in HBM: the same verdicts
+    assert verify_dev(L, bytes(mut)) == (st, blocks)
 
 
 # ---- Python view (nvlevelz_amd/framing.py) ---------------------------------

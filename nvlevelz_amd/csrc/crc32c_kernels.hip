@@ -620,6 +620,9 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
       for (int k = 0; k < 4; ++k) ov[k] = lane == 0 ? ov[k] : 0u;
     }
 #if !defined(NVL_ABL_NOREALIGN)
+    // (Unconditional -- alignbyte by 0 keeps the low word -- spares the
+    // compiler's register copies at the join but measured slower: scheduler C
+    // 10^5 x 4097 B 85.5 -> 91.5 us, config 3 223 -> 235 us, same box.)
     if (r != 0) {
       // lane 63's dword past the last piece: its edge load's e[3]
       const uint32_t nx = next_lane(w[0], ch.e[3]);
@@ -1275,19 +1278,30 @@ __device__ __forceinline__ void run_general(const G& g, const KArgs& ka, uint8_t
 // which also splits buffers across waves, ran the same chunks ~30 % slower
 // (fixed-stride: 91.7 vs 70.4 us for 10^5 x 4096 B).
 constexpr uint32_t kBufsMaxJ = 32;
+#ifndef NVL_BUFS_U
+#define NVL_BUFS_U 2  // chunks per step (1 or 2)
+#endif
 
 template <int NW, class G>
 __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* lds, uint64_t i0, uint64_t i1) {
+  NVL_STAMP0();
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nb = i1 > i0 ? i1 - i0 : 0;
-#ifndef NVL_BUFS_STATIC
-#define NVL_BUFS_STATIC 0  // 1: wave w takes groups w, w+NW, ... (contiguous, no claims)
+#ifndef NVL_BUFS_DIV
+#define NVL_BUFS_DIV 4  // about this many GS-buffer groups per wave
 #endif
-  const uint32_t GS = NVL_BUFS_STATIC
-                          ? (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, (nb + NW - 1) / NW))
-                          : (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (4u * NW)));  // buffers per group
-  const uint64_t ngroups = (nb + GS - 1) / GS;
+  const uint32_t GS = (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (NVL_BUFS_DIV * NW)));  // buffers per group
+#ifndef NVL_BUFS_TAIL
+#define NVL_BUFS_TAIL 64  // the range's last buffers go out one per group
+#endif
+  // Groups of GS buffers, then single-buffer groups for the range's last
+  // kBT buffers, so a workgroup's waves finish within about one buffer of each
+  // other (with GS-buffer groups to the end they finished 12 us apart on
+  // 10^5 x 4097 B and 27 us apart on config 3: tools/diag/bstamps.py).
+  const uint64_t kBT = NVL_BUFS_TAIL;
+  const uint64_t nbig = nb > kBT * 2 ? (nb - kBT) / GS : 0;  // GS-buffer groups
+  const uint64_t ngroups = nbig + (nb - nbig * GS);
   const uintptr_t safe = (uintptr_t)ka.tables;
 
   // the current group: lane j holds buffer gb + j (j < gn).  (Loading the
@@ -1300,18 +1314,17 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   uint64_t todo = 0;  // group lanes whose buffers have body chunks and are not started yet
   bool synced = false, done = false;
   auto load_group = [&](uint64_t k) {
-    gb = i0 + k * GS;
-    const uint32_t gn = (uint32_t)min<uint64_t>(GS, i1 - gb);
+    gb = i0 + (k < nbig ? k * GS : nbig * GS + (k - nbig));
+    const uint32_t gn = k < nbig ? GS : 1u;
     g.lane_meta(gb + (uint64_t)min<uint32_t>((uint32_t)lane, gn - 1u), lp, lL, ls);  // (every lane loads)
     const bool body = (uint32_t)lane < gn && chunks_for(lL) > (head_first(lL) ? 1u : 0u);
     todo = __ballot(body);
   };
   // claim groups until one has a body buffer (false: none left)
-  uint64_t mygrp = wv;
   auto claim = [&]() -> bool {
     while (todo == 0) {
       if (done || !synced) return false;
-      const uint64_t k = NVL_BUFS_STATIC ? (mygrp += NW) : (uint64_t)pull_unit(lds, lane);
+      const uint64_t k = pull_unit(lds, lane);
       if (k >= ngroups) {
         done = true;
         return false;
@@ -1352,12 +1365,11 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   // the chunk's loads, and hc[i] with a head-first buffer's first body chunk
   // (every lane, every time: past the end they read the table blob)
   auto load = [&](const BPos& q, Chunk& ch, uint32_t& hv) {
-    if (q.valid) {
+    const BufInfo sb{reinterpret_cast<const uint8_t*>(safe), kChunk, 1u, 0u};
+    if (q.valid)
       load_chunk<kGeneral>(q.bi, q.c, lane, ch);
-    } else {
-      BufInfo sb{reinterpret_cast<const uint8_t*>(safe), kChunk, 1u, 0u};
+    else
       load_chunk<kGeneral>(sb, 0, lane, ch);
-    }
     const bool hu = q.valid && ka.hc && q.fb == 1u && q.c == 1u;
     hv = __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)(hu ? (uintptr_t)(ka.hc + q.i)
                                                                                            : safe));
@@ -1376,6 +1388,7 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   __syncthreads();
   synced = true;
   const LaneBase lb = make_lane_base(lane);
+  NVL_STAMP1();
   if (!cur.valid) {
     BPos z{};
     z.valid = false;
@@ -1383,6 +1396,49 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
     load(cur, C, hvC);
   }
   uint32_t acc = 0u;
+  auto accumulate = [&](const BPos& q, uint32_t raw, uint32_t hv) {
+    const bool first = q.c == q.fb;
+    const bool head_in = first && q.fb == 1u && ka.hc;
+    acc = (!first || head_in) ? shift4096(lds, first ? hv : acc, lane) ^ raw : raw;
+    if (q.c + 1u == q.bi.J && lane == 0) ka.out[q.i] = finish(~acc, ka.flags);
+  };
+#if NVL_BUFS_U == 2
+  // Two consecutive chunks of the wave's stream per step (the same buffer's or
+  // two buffers'), their chains interleaved as in scheduler A, and the next
+  // two chunks' loads in flight meanwhile: twice the bytes in flight per wave.
+  // Both advances run before the loads are issued, so a group claim's
+  // metadata wait drains only the loads about to be consumed.
+  BPos cur1;
+  advance(cur, cur1);
+  Chunk C1;
+  uint32_t hvC1;
+  load(cur1, C1, hvC1);
+  while (cur.valid) {
+    BPos nx0, nx1;
+    advance(cur1, nx0);
+    advance(nx0, nx1);
+    Chunk N0, N1;
+    uint32_t hvN0, hvN1;
+    load(nx0, N0, hvN0);
+    load(nx1, N1, hvN1);
+    {
+      const BufInfo bis[2] = {cur.bi, cur1.valid ? cur1.bi : BufInfo{reinterpret_cast<const uint8_t*>(safe), kChunk, 1u, 0u}};
+      const uint32_t cs[2] = {cur.c, cur1.valid ? cur1.c : 0u};
+      const Chunk chs[2] = {C, C1};
+      uint32_t raws[2];
+      group_raw<kGeneral, 2>(lds, lb, bis, cs, lane, chs, raws);
+      accumulate(cur, raws[0], hvC);
+      if (cur1.valid) accumulate(cur1, raws[1], hvC1);
+      NVL_COUNT();
+    }
+    cur = nx0;
+    cur1 = nx1;
+    C = N0;
+    C1 = N1;
+    hvC = hvN0;
+    hvC1 = hvN1;
+  }
+#else
   while (cur.valid) {
     BPos nx;
     advance(cur, nx);
@@ -1391,15 +1447,14 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
     load(nx, N, hvN);
     uint32_t w[16], ov[4];
     build_words<kGeneral>(cur.bi, cur.c, lane, C, w, ov);
-    const uint32_t raw = chain_fold<kGeneral>(lds, lb, w, lane);
-    const bool first = cur.c == cur.fb;
-    const bool head_in = first && cur.fb == 1u && ka.hc;
-    acc = (!first || head_in) ? shift4096(lds, first ? hvC : acc, lane) ^ raw : raw;
-    if (cur.c + 1u == cur.bi.J && lane == 0) ka.out[cur.i] = finish(~acc, ka.flags);
+    accumulate(cur, chain_fold<kGeneral>(lds, lb, w, lane), hvC);
+    NVL_COUNT();
     cur = nx;
     C = N;
     hvC = hvN;
   }
+#endif
+  NVL_STAMP_END();
 }
 
 // ---------------------------------------------------------------------------

@@ -16,13 +16,15 @@ from nvlevelz_amd import _lib
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default=None); ap.add_argument("--blocks", type=int, default=100000)
 ap.add_argument("--launches", type=int, default=20); ap.add_argument("--len", type=int, default=4096)
-ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "var4097", "gen", "rand"])
+ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "var4097", "gen", "rand", "varlen"])
+ap.add_argument("--gap", type=int, default=4)  # varlen: bytes between buffers
 a = ap.parse_args()
 lib = _lib.lib
 if a.lib:
     lib = ctypes.CDLL(os.path.abspath(a.lib), mode=os.RTLD_LOCAL)
     for name, (res, args) in _lib.SIGNATURES.items():
-        f = getattr(lib, name); f.restype = res; f.argtypes = args
+        if hasattr(lib, name):
+            f = getattr(lib, name); f.restype = res; f.argtypes = args
 dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
 assert lib.nvl_crc32c_init(0) == 0
 st = torch.cuda.current_stream().cuda_stream
@@ -44,11 +46,12 @@ else:
         total, seed = 1 << 30, 0x5EED0002
     else:
         n = a.blocks
-        if a.config == "var4097":
-            lens = np.full(n, 4097, dtype=np.int64)
+        gap = a.gap if a.config == "varlen" else 4
+        if a.config in ("var4097", "varlen"):
+            lens = np.full(n, 4097 if a.config == "var4097" else a.len, dtype=np.int64)
         else:
             lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
-        offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]]).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens + gap)[:-1]]).astype(np.int64)
         total, seed = int(offs[-1] + lens[-1]) + 4, 0x5EED0001
     n = lens.size
     buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)

@@ -245,10 +245,10 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   const bool small = var_plan_small(n);
 #if !defined(NVL_NO_FUSED)
-  if (small && s->num_cu <= 4096) lc.counter = counters_for(s, st);
-  if (lc.counter) {
+  if (s->num_cu <= 1023) lc.counter = counters_for(s, st);
+  if (lc.counter) {  // (cs holds lpre, the unit map region the tiles)
     hipError_t ef = launch_var_fused(lc, static_cast<const uint8_t*>(base), offsets, lengths, n, init, init_all, out,
-                                     flags, recs, hc);
+                                     flags, recs, hc, cs, unit_first);
     if (own) (void)hipFreeAsync(ws, st);
     return hip_rc(ef);
   }

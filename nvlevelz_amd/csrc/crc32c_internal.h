@@ -69,11 +69,13 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
                       uint32_t init_all, uint32_t* out, uint32_t flags, Rec* recs, uint32_t* hc, uint32_t* long_bufs,
                       bool have_unit_map);
 
-// Plan + checksum + fix-up in one launch (n <= kPlanSmallMax, lc.counter
-// set); recs: the launch_var workspace records (hold the edge records).
+// A variable-length batch in two launches (lc.counter set): the head kernel
+// (heads + the plan's tiles: lpre[n], tiles[2 * head grid]) and the fused
+// kernel (chunk positions from the tiles, checksum, fix-up); recs: the
+// launch_var workspace records (hold the edge records).
 hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                             uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
-                            Rec* recs, uint32_t* hc);
+                            Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles);
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

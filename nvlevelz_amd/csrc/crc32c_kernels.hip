@@ -315,6 +315,14 @@ struct KArgs {
   // kBufsMaxJ chunks (set by the plan kernels); zero lets the body kernel use
   // the buffer scheduler (no split buffers).  nullptr: unknown.
   const uint32_t* long_bufs = nullptr;
+  // Variable-length plan, written by the head kernel (tile_scan) and read by
+  // the body kernel (tiled_plan).  Tile b = buffers [S*b, min(n, S*b + S)):
+  // lpre[i] = the tile-local exclusive prefix of the chunk counts,
+  // tiles[2b] = the tile's chunk total, tiles[2b+1] = its largest count.
+  uint64_t* lpre = nullptr;
+  uint64_t* tiles = nullptr;
+  uint64_t tile_S = 0;  // buffers per tile
+  uint32_t tile_G = 0;  // tiles (the head kernel's workgroups)
 };
 
 // floor(a / d) for wave-uniform a < 2^63, d > 0, from a double-precision
@@ -354,6 +362,7 @@ __device__ __forceinline__ void global_put_recs(const KArgs& ka, uint32_t u, con
 }
 
 struct FixedGeom {
+  static constexpr bool kTiled = false;  // no plan: chunk positions are arithmetic
   const uint8_t* base;
   uint64_t stride, len, n;
   uint32_t J;
@@ -388,6 +397,7 @@ struct FixedGeom {
 };
 
 struct VarGeom {
+  static constexpr bool kTiled = true;  // the head kernel writes the plan's tiles
   const uint8_t* base;
   const uint64_t* offsets;
   const uint64_t* lengths;
@@ -1590,20 +1600,117 @@ __device__ __forceinline__ uint32_t head_chain(const uint8_t* lds, const LaneBas
   return crc;
 }
 
+// Plan, part 1 (variable-length batches, in the head kernel before its LDS
+// fill, with LDS scratch under the table image): workgroup b owns tile b and
+// writes lpre/tiles (see KArgs).  Thread t takes 4 consecutive buffers per
+// step; one block-wide scan per 4096 buffers.  The body kernel's tiled_plan
+// turns the tiles into chunk positions, so a variable-length batch needs no
+// plan kernels of its own (the counts -> device scan -> unit map -> fix-up
+// launches cost ~20 us on 10^5 buffers).  Returns (block-uniform) whether
+// some buffer of the tile has a head that needs the lookup tables (4..4095
+// bytes; shorter ones are done bitwise, see bitwise_raw).
+template <int NW, class G>
+__device__ bool tile_scan(const G& g, const KArgs& ka, uint8_t* lds) {
+  constexpr uint32_t kT = kWave * NW, kPer = 4;
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(lds);           // [NW]
+  uint32_t* wmax = reinterpret_cast<uint32_t*>(lds + 8u * NW);  // [NW]
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint64_t S = ka.tile_S, lo = S * blockIdx.x;
+  const uint64_t hi = lo < g.n ? min(g.n, lo + S) : lo;
+  uint64_t carry = 0;
+  uint32_t mj = 0;
+  bool tab = false;
+  for (uint64_t base = lo; base < hi; base += (uint64_t)kT * kPer) {  // (uniform trip count)
+    const uint64_t i0 = base + (uint64_t)t * kPer;
+    uint64_t L[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) L[k] = i0 + k < hi ? g.lengths[i0 + k] : 0;
+    uint32_t J[kPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      J[k] = i0 + k < hi ? chunks_for(L[k]) : 0u;
+      sum += J[k];
+      mj = max(mj, J[k]);
+      const uint64_t hl = L[k] - (uint64_t)kChunk * (J[k] - 1u);
+      tab |= i0 + k < hi && L[k] >= 4 && hl >= 4 && hl < kChunk;
+    }
+    uint64_t x = sum;  // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)NW; ++v) {
+      const uint64_t sv = wsum[v];
+      before += v < wv ? sv : 0;
+      tot += sv;
+    }
+    uint64_t e = carry + before + x - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      if (i0 + k < hi) ka.lpre[i0 + k] = e;
+      e += J[k];
+    }
+    carry += tot;
+    __syncthreads();  // (wsum is rewritten by the next step)
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mj = max(mj, (uint32_t)__shfl_xor((int)mj, o));
+  if (lane == 0) wmax[wv] = mj;
+  const bool need = __syncthreads_or(tab ? 1 : 0) != 0;
+  if (t == 0) {
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)NW; ++v) m = max(m, wmax[v]);
+    ka.tiles[2ull * blockIdx.x] = carry;
+    ka.tiles[2ull * blockIdx.x + 1] = m;
+  }
+  __syncthreads();  // (the scratch becomes the table image)
+  return need;
+}
+
+// CRC register after n <= 3 bytes at p from state l, bit by bit (the
+// reflected polynomial, util/crc32c.cc:287 STEP1 semantics): no tables, so a
+// workgroup whose heads are all this short skips its 156 KiB LDS fill
+// (10^5 x 4097 B: every head is 1 byte).
+__device__ __forceinline__ uint32_t bitwise_raw(const uint8_t* p, uint32_t n, uint32_t l) {
+  for (uint32_t k = 0; k < n; ++k) {
+    l ^= (uint32_t)p[k];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) l = (l >> 1) ^ (0x82F63B78u & (0u - (l & 1u)));
+  }
+  return l;
+}
+
 template <class G>
 __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerWG;
-  const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerWG + wv;
-  const uint64_t b0 = g.n * gw / nwaves, b1 = g.n * (gw + 1) / nwaves;
+  // the workgroup's buffers: its plan tile when there is one
+  uint64_t w0 = g.n * blockIdx.x / gridDim.x, w1 = g.n * (blockIdx.x + 1) / gridDim.x;
+  bool tables = true;
+  if constexpr (G::kTiled) {
+    if (ka.lpre) {
+      tables = tile_scan<kWavesPerWG>(g, ka, lds);
+      w0 = min(g.n, ka.tile_S * blockIdx.x);
+      w1 = min(g.n, w0 + ka.tile_S);
+    }
+  }
+  const uint64_t b0 = w0 + (w1 - w0) * wv / kWavesPerWG, b1 = w0 + (w1 - w0) * (wv + 1) / kWavesPerWG;
   const LaneBase lb = make_lane_base(lane);
   uintptr_t lp = 0;  // the lane's buffer of the current group: start, length, ~init
   uint64_t lL = 0;
   uint32_t ls = 0;
   if (b0 + (uint64_t)lane < b1) g.lane_meta(b0 + (uint64_t)lane, lp, lL, ls);  // in flight during the fill
-  fill_lds<kWavesPerWG>(lds, ka.tables);
-  __syncthreads();
+  if (tables) {
+    fill_lds<kWavesPerWG>(lds, ka.tables);
+    __syncthreads();
+  }
   for (uint64_t gb = b0; gb < b1; gb += kWave) {
     const bool valid = gb + (uint64_t)lane < b1;
     const uint64_t i = gb + (uint64_t)lane;
@@ -1616,18 +1723,15 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     const bool tiny = valid && lL < 4;
     const uint32_t J = chunks_for(lL);
     const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);  // first chunk's bytes
-    const bool head = valid && !tiny && hl < kChunk;
+    const bool shrt = valid && !tiny && hl < 4;               // 1..3-byte head of a longer buffer
+    const bool head = valid && !tiny && !shrt && hl < kChunk;
     const uint32_t cls = hl <= 64u ? 0u : (hl <= 256u ? 1u : (hl <= 1024u ? 2u : 3u));
     // what setup pulls across lanes: head bytes (< 4096) | kHeadLast << 16
     const uint32_t hlx = (uint32_t)(hl & 0xFFFFu) | (J == 1u ? kHeadLast << 16 : 0u);
-    if (tiny) {
-      uint32_t l = ls;  // = ~init
-      for (uint32_t k = 0; k < (uint32_t)lL; ++k) {
-        const uint32_t by = reinterpret_cast<const uint8_t*>(lp)[k];
-        l = lds_u32(lds + kSliceOff, (((l ^ by) & 0xFFu) << 8) | ((uint32_t)(lane & 31) << 2)) ^ (l >> 8);  // T0
-      }
-      ka.out[i] = finish(~l, ka.flags);
-    }
+    if (tiny) ka.out[i] = finish(~bitwise_raw(reinterpret_cast<const uint8_t*>(lp), (uint32_t)lL, ls), ka.flags);
+    // hc = raw(0, head ^ s's low bytes) = raw(s, head) ^ (s >> 8 hl): the body
+    // injects s's remaining bytes into its first word itself
+    if (shrt) ka.hc[i] = bitwise_raw(reinterpret_cast<const uint8_t*>(lp), (uint32_t)hl, ls) ^ (ls >> (8u * (uint32_t)hl));
     uint64_t m[4];
     uint32_t nr[4], NR = 0;
 #pragma unroll
@@ -2008,6 +2112,7 @@ struct VarGeomFused {
   }
 };
 
+
 #if defined(NVL_DIAG_FUSED)
 __device__ unsigned long long g_fstamps[8 * 1024];
 #define NVL_FSTAMP(k) \
@@ -2016,55 +2121,42 @@ __device__ unsigned long long g_fstamps[8 * 1024];
 #define NVL_FSTAMP(k) do {} while (0)
 #endif
 
-// Plan prologue.  After it: LDS holds ubuf/uc for the 64 local units, and
-// C0/C1 (returned) bound the workgroup's chunk range.
+// Plan, part 2, from the head kernel's tiles (tile_scan), in the LDS the
+// tables later occupy: the tile totals' block scan gives each tile's first
+// chunk (tb[], T = tb[Gt]); the workgroup's chunk range is [T*b/G, T*(b+1)/G).
+// Chunk q lies in the last tile k with tb[k] <= q (binary search in LDS) and
+// there in the last buffer a with tb[k] + lpre[a] <= q: a 16-ary search over
+// lpre by 16 lanes (ballot of the 16 probes), about log16(S) rounds of
+// global loads.  Scheduler B needs the first chunk of each of the 64 units
+// (64 searches, 16 lanes each: the whole block); scheduler C only the first
+// buffers starting at or after C0 and C1 (2 searches).
+constexpr uint32_t kMaxTiles = 1023;
+constexpr uint32_t kTbWsumOff = 8u * (kMaxTiles + 1u);  // u64 [16]
+constexpr uint32_t kTbResOff = kTbWsumOff + 16u * 8u;   // u64 B0, B1
+static_assert(kTbResOff + 16u <= kSliceOff + kRepBytes, "tiled plan scratch must fit under the table image");
+
 template <int NW>
-__device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restrict__ lengths, uint32_t nn,
-                                           uint64_t& C0, uint64_t& C1, bool& long_bufs, uint64_t& B0,
-                                           uint64_t& B1) {
+__device__ __forceinline__ void tiled_plan(uint8_t* lds, const VarGeom& g, const KArgs& ka, uint64_t& C0,
+                                           uint64_t& C1, bool& long_bufs, uint64_t& B0, uint64_t& B1) {
   constexpr uint32_t kT = kWave * NW;
-  static_assert(kT <= 1024 && kPlanSmallMax % kT == 0, "plan layout assumes <= 1024 threads");
-  constexpr int kPer = (int)(kPlanSmallMax / kT);
-  uint32_t* js = reinterpret_cast<uint32_t*>(lds);
-  uint64_t* wsum = reinterpret_cast<uint64_t*>(lds + kPlanWsumOff);
-  uint64_t* rstart = reinterpret_cast<uint64_t*>(lds + kPlanRunOff);
+  static_assert(kT == 1024, "64 searches of 16 lanes fill the block");
+  uint64_t* tb = reinterpret_cast<uint64_t*>(lds);
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(lds + kTbWsumOff);
+  uint64_t* res = reinterpret_cast<uint64_t*>(lds + kTbResOff);
   uint32_t* ubuf = reinterpret_cast<uint32_t*>(lds + kUnitOff);
   uint32_t* uc = ubuf + kUnitsPerWG;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  {  // chunk counts, all of the thread's lengths in flight at once
-    uint64_t Ls[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = t + (uint32_t)k * kT;
-      Ls[k] = i < nn ? lengths[i] : 0;
-    }
-    bool lng = false;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = t + (uint32_t)k * kT;
-      const uint32_t J = chunks_for(Ls[k]);
-      lng |= J > kBufsMaxJ;
-      if (i < nn) js[plan_pad(i)] = J;
-    }
-    long_bufs = __syncthreads_or(lng ? 1 : 0) != 0;
-  }
-  NVL_FSTAMP(4);
-  const uint32_t per = (nn + kT - 1) / kT;
-  const uint32_t i0 = min(nn, t * per), i1 = min(nn, i0 + per);
-  uint32_t sum = 0;  // run-relative exclusive prefixes in place
-  for (uint32_t i = i0; i < i1; ++i) {
-    const uint32_t j = js[plan_pad(i)];
-    js[plan_pad(i)] = sum;
-    sum += j;
-  }
-  uint64_t x = sum;
+  const uint32_t Gt = ka.tile_G;  // <= kMaxTiles (host)
+  const uint64_t tot = t < Gt ? ka.tiles[2ull * t] : 0;
+  const uint64_t mj = t < Gt ? ka.tiles[2ull * t + 1] : 0;
+  long_bufs = __syncthreads_or(mj > kBufsMaxJ ? 1 : 0) != 0;
+  uint64_t x = tot;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint64_t y = __shfl_up(x, o, 64);
     if (lane >= (uint32_t)o) x += y;
   }
   if (lane == 63) wsum[wv] = x;
-  NVL_FSTAMP(5);
   __syncthreads();
   uint64_t before = 0, T = 0;
 #pragma unroll
@@ -2073,50 +2165,51 @@ __device__ __forceinline__ void fused_plan(uint8_t* lds, const uint64_t* __restr
     before += v < wv ? sv : 0;
     T += sv;
   }
-  rstart[t] = before + x - sum;  // chunk_start of the run's first buffer (runs past n: T)
+  if (t <= Gt) tb[t] = before + x - tot;  // tb[Gt] = T
   __syncthreads();
-  NVL_FSTAMP(6);
-  // chunk_start of the buffer holding chunk q (q < T): last run r with
-  // rstart[r] <= q (empty runs share their successor's start, so take the
-  // last), then the last buffer of the run whose start is <= q.
-  auto buf_of = [&](uint64_t q, uint64_t& cs) -> uint32_t {
-    uint32_t lo = 0, hi = kT;  // rstart[lo] <= q < rstart[hi] (rstart[kT] := inf)
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (rstart[mid] <= q) lo = mid; else hi = mid;
-    }
-    const uint64_t r0 = rstart[lo];
-    uint32_t a = lo * per, b = min(nn, a + per);  // js[a] = 0 <= q - r0
-    while (b - a > 1) {
-      const uint32_t mid = (a + b) >> 1;
-      if (r0 + js[plan_pad(mid)] <= q) a = mid; else b = mid;
-    }
-    cs = r0 + js[plan_pad(a)];
-    return a;
-  };
-  // T is the same in every lane: keep it and the range in SGPRs (as VGPRs
-  // they stayed live through the main loop, which then spilled).
+  NVL_FSTAMP(4);
   T = uniform_u64(T);
   C0 = T * blockIdx.x / gridDim.x;
   C1 = T * (blockIdx.x + 1) / gridDim.x;
-  if (t < kUnitsPerWG) {
-    const uint64_t q = C0 + (C1 - C0) * t / kUnitsPerWG;
-    if (q < C1) {
-      uint64_t cs;
-      ubuf[t] = buf_of(q, cs);
-      uc[t] = (uint32_t)(q - cs);
+  const uint32_t s = t >> 4, j = t & 15u;  // search s, probe lane j
+  const uint32_t nsearch = long_bufs ? kUnitsPerWG : 2u;
+  if (s < nsearch) {
+    const uint64_t q = long_bufs ? C0 + (C1 - C0) * s / kUnitsPerWG : (s == 0 ? C0 : C1);
+    if (q < T && (!long_bufs || q < C1)) {
+      uint32_t klo = 0, khi = Gt;  // tb[klo] <= q < tb[khi]
+      while (khi - klo > 1) {
+        const uint32_t mid = (klo + khi) >> 1;
+        if (tb[mid] <= q) klo = mid; else khi = mid;
+      }
+      const uint64_t kb = tb[klo];
+      const uint64_t S = ka.tile_S;
+      uint64_t lo = S * klo, hi = min(g.n, lo + S);  // kb + lpre[lo] = kb <= q
+      while (hi - lo > 1) {  // (the same trip count in the group's 16 lanes)
+        const uint64_t step = (hi - lo + 15u) / 16u;
+        const uint64_t a = lo + step * j;
+        const bool le = a < hi && kb + ka.lpre[a] <= q;
+        const uint32_t bits = (uint32_t)(__ballot(le) >> (lane & 48u)) & 0xFFFFu;
+        lo += step * (uint64_t)(__builtin_popcount(bits) - 1);
+        hi = min(hi, lo + step);
+      }
+      const uint64_t key = kb + ka.lpre[lo];
+      if (j == 0) {
+        if (long_bufs) {
+          ubuf[s] = (uint32_t)lo;
+          uc[s] = (uint32_t)(q - key);
+        } else {
+          res[s] = key == q ? lo : lo + 1u;
+        }
+      }
+    } else if (j == 0 && !long_bufs) {
+      res[s] = g.n;
     }
   }
-  // scheduler C: the buffers that start in [C0, C1) (every lane the same)
-  auto first_from = [&](uint64_t q) -> uint64_t {
-    if (q >= T) return nn;
-    uint64_t cs;
-    const uint32_t b = buf_of(q, cs);
-    return cs == q ? b : b + 1u;
-  };
-  B0 = long_bufs ? 0 : first_from(C0);
-  B1 = long_bufs ? 0 : first_from(C1);
   __syncthreads();
+  NVL_FSTAMP(5);
+  B0 = long_bufs ? 0 : res[0];
+  B1 = long_bufs ? 0 : res[1];
+  __syncthreads();  // (the scratch becomes the table image)
 }
 
 // XOR into `total` the earlier portions of buffer `buf` (LDS records of units
@@ -2160,7 +2253,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1, B0, B1;
   bool long_bufs;
-  fused_plan<kGenWaves>(lds, gv.lengths, (uint32_t)gv.n, C0, C1, long_bufs, B0, B1);
+  tiled_plan<kGenWaves>(lds, gv, ka, C0, C1, long_bufs, B0, B1);
   // The range is uniform, but the 64-bit divisions that made it ran on the
   // VALU: pin it to SGPRs, or it stays in VGPRs through the main loop and
   // that spills (25 VGPRs, 108 B/lane scratch, cfg3 287 -> 430 us).
@@ -2321,13 +2414,22 @@ static inline uint32_t chunks_of(uint64_t len) { return dev::chunks_for(len); }
 
 // The head kernel over a geometry's n buffers; its dispatch records
 // ev_start when given (it is then the call's first kernel).
+static inline uint32_t head_grid(int num_cu, uint64_t n) {
+  const uint64_t per_wg = 8u * dev::kWavesPerWG;  // at least ~8 buffers per wave
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_cu, (n + per_wg - 1) / per_wg));
+}
+
 template <class G>
 static hipError_t launch_heads(const LaunchCtx& lc, const G& g, uint32_t* out, uint32_t flags, uint32_t* hc,
-                               hipEvent_t ev_start) {
-  const uint64_t per_wg = 8u * dev::kWavesPerWG;  // at least ~8 buffers per wave
-  const uint32_t grid =
-      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)lc.num_cu, (g.n + per_wg - 1) / per_wg));
-  const dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, hc};
+                               hipEvent_t ev_start, uint64_t* lpre = nullptr, uint64_t* tiles = nullptr) {
+  const uint32_t grid = head_grid(lc.num_cu, g.n);
+  dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, hc};
+  if (lpre) {  // tiles of the variable-length plan: one per workgroup
+    ka.lpre = lpre;
+    ka.tiles = tiles;
+    ka.tile_G = grid;
+    ka.tile_S = (g.n + grid - 1) / grid;
+  }
   if (ev_start)
     hipExtLaunchKernelGGL(dev::crc32c_head_kernel<G>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, ev_start,
                           nullptr, 0u, g, ka);
@@ -2413,13 +2515,17 @@ bool var_plan_small(uint64_t n) { return n <= dev::kPlanSmallMax; }
 
 hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                             uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
-                            Rec* recs, uint32_t* hc) {
+                            Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles) {
   if (n == 0) return hipSuccess;
-  if (n > dev::kPlanSmallMax || !lc.counter || lc.num_cu > (int)dev::kMaxFusedGrid) return hipErrorInvalidValue;
+  if (!lc.counter || !lpre || !tiles || lc.num_cu > (int)dev::kMaxTiles) return hipErrorInvalidValue;
   dev::VarGeom g{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
-  hipError_t eh = launch_heads(lc, g, out, flags, hc, nullptr);
+  hipError_t eh = launch_heads(lc, g, out, flags, hc, nullptr, lpre, tiles);
   if (eh != hipSuccess) return eh;
   dev::KArgs ka{out, flags, recs, lc.tables, lc.counter, hc};
+  ka.lpre = lpre;
+  ka.tiles = tiles;
+  ka.tile_G = head_grid(lc.num_cu, n);
+  ka.tile_S = (n + ka.tile_G - 1) / ka.tile_G;
   hipLaunchKernelGGL(dev::crc32c_var_fused_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kWave * dev::kGenWaves), 0,
                      lc.stream, g, ka);
   return hipGetLastError();

@@ -11,8 +11,13 @@ for name, (res, args) in _lib.SIGNATURES.items():
 dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
 assert lib.nvl_crc32c_init(0) == 0
 g = json.load(open(os.path.join(R, "tests", "golden", "configs.json")))["cfg3"]
-lens = oracle.port().cfg3_lengths(g["len_seed"], g["total"])
-offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64); n = lens.size
+if os.environ.get("CFG", "3") == "v":  # 10^5 x 4097 B at stride 4101
+    lens = np.full(100_000, 4097, dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]]).astype(np.int64); n = lens.size
+    g = dict(g, total=int(offs[-1] + lens[-1]) + 4, digest=None)
+else:
+    lens = oracle.port().cfg3_lengths(g["len_seed"], g["total"])
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64); n = lens.size
 buf = torch.empty(g["total"] + 64, dtype=torch.uint8, device=dev)
 lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (g["total"] + 64) // 8, 8, 0, 1, g["seed"], None)
 o = torch.from_numpy(offs).to(dev); m = torch.from_numpy(lens.astype(np.int64)).to(dev)
@@ -38,8 +43,9 @@ print("last WG end (us after first start):", (last[:, 7] - h[:, 0].min()) / 100.
 h[h[:, 7] == 0, 7] = h[h[:, 7] > 0, 7].max() if (h[:, 7] > 0).any() else 0
 t0 = h[:, 0].min()
 us = (h - t0) / 100.0
-for k, name in enumerate(["start", "plan_done", "units_done", "counted", "counts", "runwalk_t0", "scan_sync", "last_end"]):
+for k, name in enumerate(["start", "plan_done", "units_done", "counted", "4", "5", "6", "last_end"]):
     q = np.percentile(us[:, k], [0, 10, 50, 90, 100])
     print(f"{name:11s}", " ".join(f"{x:8.2f}" for x in q))
 print("plan duration p50/max:", np.median(us[:, 1] - us[:, 0]), (us[:, 1] - us[:, 0]).max())
-print("digest ok:", oracle.port().digest(out.cpu().numpy().view(np.uint32)) == g["digest"])
+if g["digest"] is not None:
+    print("digest ok:", oracle.port().digest(out.cpu().numpy().view(np.uint32)) == g["digest"])

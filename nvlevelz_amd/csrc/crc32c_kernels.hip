@@ -255,7 +255,7 @@ __device__ __forceinline__ uint32_t shift4096(const uint8_t* lds, uint32_t acc, 
 
 // Fill the LDS image from the device table blob.
 template <int NW>
-__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restrict__ g) {
+__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restrict__ g, uint32_t ctr0 = NW) {
   constexpr int kT = kWave * NW;
   const int t = threadIdx.x;
   // replicated slice tables: 8192 16-byte stores, consecutive lanes write
@@ -274,7 +274,7 @@ __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restric
   const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
   uint4* dst = reinterpret_cast<uint4*>(lds + kCombOff);
   for (int q = t; q < 1792; q += kT) dst[q] = src[q];
-  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = (uint32_t)NW;  // units 0..NW-1 are pre-assigned
+  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = ctr0;  // units 0..ctr0-1 are pre-assigned
 }
 
 __device__ __forceinline__ uint32_t finish(uint32_t crc, uint32_t flags) {
@@ -1288,9 +1288,52 @@ __device__ __forceinline__ void run_general(const G& g, const KArgs& ka, uint8_t
 // which also splits buffers across waves, ran the same chunks ~30 % slower
 // (fixed-stride: 91.7 vs 70.4 us for 10^5 x 4096 B).
 constexpr uint32_t kBufsMaxJ = 32;
-#ifndef NVL_BUFS_U
-#define NVL_BUFS_U 2  // chunks per step (1 or 2)
-#endif
+
+// A chunk of scheduler C's stream, wave-uniform (SGPRs): where it ends, its
+// buffer, the buffer's ~init and what the chunk is to its buffer.
+struct CPos {
+  uintptr_t ce;  // chunk end (an invalid position: safe + 4096, the loads read the table blob)
+  uint64_t i;    // buffer index
+  uint32_t s;    // ~init
+  uint32_t f;    // kPos* flags | inj << 8: inj = (chunk start - buffer start) when < 4 (~init lands there), else 0xFF
+};
+constexpr uint32_t kPosValid = 1u, kPosFirst = 2u, kPosLast = 4u, kPosHeadIn = 8u;
+
+// The chunk's four row loads from A4 (the 4-byte aligned address at or below
+// the chunk start), the edge dword (see Chunk), and hc[i] when the chunk is a
+// head-first buffer's first body chunk (the table blob otherwise): the same
+// loads for every position, valid or not, so the wait counts stay exact.
+__device__ __forceinline__ void load_pos(const CPos& q, int lane, uintptr_t safe, const uint32_t* hc, Chunk& ch,
+                                         uint32_t& hv) {
+  const uint32_t r = (uint32_t)(q.ce & 3u);
+  const uintptr_t A4 = q.ce - kChunk - r;
+  const uint32_t lo = lane_load_off(lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
+    ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+  }
+  ch.e[3] = *(const __attribute__((address_space(1))) uint32_t*)(A4 + (r ? kChunk : kChunk - 4u));
+  const uintptr_t ha = (q.f & kPosHeadIn) ? (uintptr_t)(hc + q.i) : safe;
+  hv = __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)ha);
+}
+
+// The lane's 16 words of piece P = lane of the chunk (build_words<kGeneral>
+// from scalars): transpose, realign by r = ce & 3, ~init at the buffer start.
+__device__ __forceinline__ void build_pos(const CPos& q, int lane, const Chunk& ch, uint32_t (&w)[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
+  row_transpose(w);
+  const uint32_t r = (uint32_t)(q.ce & 3u);
+  if (r != 0) {
+    const uint32_t nx = next_lane(w[0], ch.e[3]);
+#pragma unroll
+    for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+    w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
+  }
+  const uint32_t inj = q.f >> 8;
+  if (inj < 4u && lane == 0) w[0] ^= q.s >> (8u * inj);
+}
 
 template <int NW, class G>
 __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* lds, uint64_t i0, uint64_t i1) {
@@ -1314,156 +1357,148 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   const uint64_t ngroups = nbig + (nb - nbig * GS);
   const uintptr_t safe = (uintptr_t)ka.tables;
 
-  // the current group: lane j holds buffer gb + j (j < gn).  (Loading the
-  // next group's metadata one group ahead measured slower: 95 -> 101 us on
-  // 10^5 x 4097 B, the copies at adoption wait on the loads in flight.)
-  uint64_t gb = 0;
+  // Groups: the current one (lane j holds buffer gb + j: start, length,
+  // ~init) and the next one, claimed and its metadata loads issued one
+  // iteration ahead.  Every iteration first builds the words of the chunks
+  // in hand (waiting for their loads, which were issued AFTER the next
+  // group's metadata), then adopts groups and issues the next loads: an
+  // adoption never waits on a load still in flight.  fill_lds starts the LDS
+  // counter at 2 * NW: groups wv and NW + wv are pre-assigned.
+  uint64_t gb = 0, todo = 0;  // todo: group lanes whose buffers have body chunks, not started
   uintptr_t lp = 0;
   uint64_t lL = 0;
   uint32_t ls = 0;
-  uint64_t todo = 0;  // group lanes whose buffers have body chunks and are not started yet
-  bool synced = false, done = false;
-  auto load_group = [&](uint64_t k) {
-    gb = i0 + (k < nbig ? k * GS : nbig * GS + (k - nbig));
-    const uint32_t gn = k < nbig ? GS : 1u;
-    g.lane_meta(gb + (uint64_t)min<uint32_t>((uint32_t)lane, gn - 1u), lp, lL, ls);  // (every lane loads)
-    const bool body = (uint32_t)lane < gn && chunks_for(lL) > (head_first(lL) ? 1u : 0u);
-    todo = __ballot(body);
+  uint64_t ngb = 0;
+  uint32_t ngn = 0;
+  bool has_nxt = false, nxt_ready = false;
+  // The next group's raw metadata, reloaded by EVERY iteration at one place
+  // (meta_load, before the chunk loads): the loads are unconditional and
+  // nothing is computed from them until the adoption, so they never need a
+  // copy at a control-flow join -- such a copy waits for the load (with
+  // conditional loads the compiler waited right after issuing them).
+  uint64_t no = 0, nL = 0;
+  uint32_t ni = 0;
+  auto claim_group = [&](uint64_t k) {  // the next group's index (scalars only)
+    has_nxt = k < ngroups;
+    nxt_ready = false;
+    ngb = has_nxt ? i0 + (k < nbig ? k * GS : nbig * GS + (k - nbig)) : 0u;
+    ngn = has_nxt ? (k < nbig ? GS : 1u) : 1u;
   };
-  // claim groups until one has a body buffer (false: none left)
-  auto claim = [&]() -> bool {
-    while (todo == 0) {
-      if (done || !synced) return false;
-      const uint64_t k = pull_unit(lds, lane);
-      if (k >= ngroups) {
-        done = true;
-        return false;
+  const uint32_t* const ibase = g.init ? g.init : reinterpret_cast<const uint32_t*>(safe);
+  auto meta_load = [&]() {
+    const uint64_t i = ngb + (uint64_t)min<uint32_t>((uint32_t)lane, ngn - 1u);  // < n (buffer 0 when none)
+    no = g.offsets[i];
+    nL = g.lengths[i];
+    ni = ibase[g.init ? i : 0u];
+  };
+  auto adopt = [&]() {
+    lp = (uintptr_t)g.base + no;
+    lL = nL;
+    ls = ~(g.init ? ni : g.init_all);
+    gb = ngb;
+    todo = __ballot((uint32_t)lane < ngn && chunks_for(lL) > (head_first(lL) ? 1u : 0u));
+    has_nxt = false;
+  };
+  // the buffer being walked
+  uintptr_t cp = 0;
+  uint64_t cL = 0, ci = 0;
+  uint32_t cJ = 0, cx = 0, cc = 0, cfb = 0;
+  bool cvalid = false;
+  // the stream's next chunk (invalid when the work is done or the next group
+  // is not in registers yet)
+  auto next_pos = [&](CPos& q) {
+    q.ce = safe + kChunk;
+    q.i = 0;
+    q.s = 0;
+    q.f = 0;
+    if (cvalid && cc + 1u < cJ) {
+      ++cc;
+    } else {
+      cvalid = false;
+      while (todo == 0) {
+        if (!has_nxt || !nxt_ready) return;
+        adopt();
+        claim_group(pull_unit(lds, lane));  // its metadata: this iteration's meta_load
       }
-      load_group(k);
+      const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1u;
+      cp = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lp >> 32), (int)j) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lp, (int)j);
+      cL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lL >> 32), (int)j) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lL, (int)j);
+      cx = (uint32_t)__builtin_amdgcn_readlane((int)ls, (int)j);
+      ci = gb + j;
+      cJ = chunks_for(cL);
+      cfb = head_first(cL) ? 1u : 0u;
+      cc = cfb;
+      cvalid = true;
     }
-    return true;
+    q.ce = cp + cL - (uint64_t)kChunk * (cJ - 1u - cc);
+    q.i = ci;
+    q.s = cx;
+    const uintptr_t cs = q.ce - kChunk;  // >= cp: body chunks start at or after the buffer start
+    const uint32_t inj = cs < cp + 4u ? (uint32_t)(cs - cp) : 0xFFu;
+    q.f = kPosValid | (cc == cfb ? kPosFirst : 0u) | (cc + 1u == cJ ? kPosLast : 0u) |
+          (cc == cfb && cfb == 1u && ka.hc ? kPosHeadIn : 0u) | (inj << 8);
   };
-  struct BPos {
-    BufInfo bi;
-    uint64_t i;
-    uint32_t c, fb;
-    bool valid;
-  };
-  auto start_buffer = [&](BPos& q) {
-    const uint32_t j = (uint32_t)__builtin_ctzll(todo);
-    todo &= todo - 1u;
-    const uintptr_t p = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lp >> 32), (int)j) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lp, (int)j);
-    const uint64_t L = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lL >> 32), (int)j) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lL, (int)j);
-    const uint32_t sx = (uint32_t)__builtin_amdgcn_readlane((int)ls, (int)j);
-    q.bi = BufInfo{reinterpret_cast<const uint8_t*>(p), L, chunks_for(L), sx};
-    q.i = gb + j;
-    q.fb = head_first(L) ? 1u : 0u;
-    q.c = q.fb;
-    q.valid = true;
-  };
-  auto advance = [&](const BPos& cur, BPos& nx) {
-    nx = cur;
-    if (cur.valid && cur.c + 1u < cur.bi.J) {
-      nx.c = cur.c + 1u;
-      return;
-    }
-    nx.valid = false;
-    if (todo != 0 || claim()) start_buffer(nx);
-  };
-  // the chunk's loads, and hc[i] with a head-first buffer's first body chunk
-  // (every lane, every time: past the end they read the table blob)
-  auto load = [&](const BPos& q, Chunk& ch, uint32_t& hv) {
-    const BufInfo sb{reinterpret_cast<const uint8_t*>(safe), kChunk, 1u, 0u};
-    if (q.valid)
-      load_chunk<kGeneral>(q.bi, q.c, lane, ch);
-    else
-      load_chunk<kGeneral>(sb, 0, lane, ch);
-    const bool hu = q.valid && ka.hc && q.fb == 1u && q.c == 1u;
-    hv = __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)(hu ? (uintptr_t)(ka.hc + q.i)
-                                                                                           : safe));
-  };
+  auto more = [&]() -> bool { return (cvalid && cc + 1u < cJ) || todo != 0 || has_nxt; };
 
-  BPos cur{};
-  cur.valid = false;
-  Chunk C;
-  uint32_t hvC = 0u;
-  if (wv < ngroups) {  // the pre-assigned first group (fill_lds starts the counter at NW)
-    load_group(wv);
-    if (todo) start_buffer(cur);
-  }
-  load(cur, C, hvC);  // overlaps the LDS fill
-  fill_lds<NW>(lds, ka.tables);
+  // pre-assigned: group wv now, group NW + wv as the next one
+  claim_group(wv);
+  meta_load();
+  if (has_nxt) adopt();
+  claim_group(NW + wv);
+  meta_load();
+  CPos p0, p1;
+  next_pos(p0);  // (no adoption before the barrier: the next group is not ready)
+  next_pos(p1);
+  Chunk c0, c1;
+  uint32_t hv0, hv1;
+  load_pos(p0, lane, safe, ka.hc, c0, hv0);  // overlaps the LDS fill
+  load_pos(p1, lane, safe, ka.hc, c1, hv1);
+  fill_lds<NW>(lds, ka.tables, 2u * NW);
   __syncthreads();
-  synced = true;
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();
-  if (!cur.valid) {
-    BPos z{};
-    z.valid = false;
-    advance(z, cur);
-    load(cur, C, hvC);
-  }
   uint32_t acc = 0u;
-  auto accumulate = [&](const BPos& q, uint32_t raw, uint32_t hv) {
-    const bool first = q.c == q.fb;
-    const bool head_in = first && q.fb == 1u && ka.hc;
-    acc = (!first || head_in) ? shift4096(lds, first ? hv : acc, lane) ^ raw : raw;
-    if (q.c + 1u == q.bi.J && lane == 0) ka.out[q.i] = finish(~acc, ka.flags);
+  // hs: shift4096 of the buffer's head register (hc[i]) for a first body chunk
+  auto accumulate = [&](const CPos& q, uint32_t raw, uint32_t hs) {
+    const bool first = (q.f & kPosFirst) != 0u;
+    acc = (first ? ((q.f & kPosHeadIn) ? hs : 0u) : shift4096(lds, acc, lane)) ^ raw;
+    if ((q.f & kPosLast) && lane == 0) ka.out[q.i] = finish(~acc, ka.flags);
   };
-#if NVL_BUFS_U == 2
   // Two consecutive chunks of the wave's stream per step (the same buffer's or
-  // two buffers'), their chains interleaved as in scheduler A, and the next
-  // two chunks' loads in flight meanwhile: twice the bytes in flight per wave.
-  // Both advances run before the loads are issued, so a group claim's
-  // metadata wait drains only the loads about to be consumed.
-  BPos cur1;
-  advance(cur, cur1);
-  Chunk C1;
-  uint32_t hvC1;
-  load(cur1, C1, hvC1);
-  while (cur.valid) {
-    BPos nx0, nx1;
-    advance(cur1, nx0);
-    advance(nx0, nx1);
-    Chunk N0, N1;
-    uint32_t hvN0, hvN1;
-    load(nx0, N0, hvN0);
-    load(nx1, N1, hvN1);
-    {
-      const BufInfo bis[2] = {cur.bi, cur1.valid ? cur1.bi : BufInfo{reinterpret_cast<const uint8_t*>(safe), kChunk, 1u, 0u}};
-      const uint32_t cs[2] = {cur.c, cur1.valid ? cur1.c : 0u};
-      const Chunk chs[2] = {C, C1};
+  // two buffers'), their chains interleaved as in scheduler A.  The step's
+  // words are built and its head registers shifted first (c0/c1, hv0/hv1
+  // die), then the next two chunks' loads go out into the same registers,
+  // then the chains run: no register copies at the loop's back edge (a copy
+  // of a loaded register waits for the load).
+  while (true) {
+    nxt_ready = has_nxt;  // its metadata was loaded before the chunk loads built below
+    uint32_t w[2][16];
+    const bool work = (p0.f & kPosValid) != 0u;
+    if (work) {
+      build_pos(p0, lane, c0, w[0]);
+      build_pos(p1, lane, c1, w[1]);
+    }
+    const uint32_t hs0 = shift4096(lds, hv0, lane), hs1 = shift4096(lds, hv1, lane);
+    CPos q0, q1;
+    next_pos(q0);
+    next_pos(q1);
+    meta_load();
+    load_pos(q0, lane, safe, ka.hc, c0, hv0);
+    load_pos(q1, lane, safe, ka.hc, c1, hv1);
+    if (work) {
       uint32_t raws[2];
-      group_raw<kGeneral, 2>(lds, lb, bis, cs, lane, chs, raws);
-      accumulate(cur, raws[0], hvC);
-      if (cur1.valid) accumulate(cur1, raws[1], hvC1);
+      chains<2, false>(lds, lb, w, lane, raws);
+      accumulate(p0, raws[0], hs0);
+      if (p1.f & kPosValid) accumulate(p1, raws[1], hs1);
       NVL_COUNT();
     }
-    cur = nx0;
-    cur1 = nx1;
-    C = N0;
-    C1 = N1;
-    hvC = hvN0;
-    hvC1 = hvN1;
+    if (!(q0.f & kPosValid) && !more()) break;
+    p0 = q0;
+    p1 = q1;
   }
-#else
-  while (cur.valid) {
-    BPos nx;
-    advance(cur, nx);
-    Chunk N;
-    uint32_t hvN;
-    load(nx, N, hvN);
-    uint32_t w[16], ov[4];
-    build_words<kGeneral>(cur.bi, cur.c, lane, C, w, ov);
-    accumulate(cur, chain_fold<kGeneral>(lds, lb, w, lane), hvC);
-    NVL_COUNT();
-    cur = nx;
-    C = N;
-    hvC = hvN;
-  }
-#endif
   NVL_STAMP_END();
 }
 
@@ -2264,13 +2299,13 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,
                        ubuf + kUnitsPerWG, ub0};
   if (NVL_VAR_BUFS && !long_bufs) {
-    // whole buffers: no unit records, so no edge records either
-    Rec* lr0 = reinterpret_cast<Rec*>(lds + kRecOff);
-    if (threadIdx.x < 2 * kUnitsPerWG) lr0[threadIdx.x] = Rec{kNoBuf, 0u, 0u};
+    // whole buffers: no records, so no edge fold either -- no grid-wide
+    // hand-off (its sc1 stores, drain and counter round trip cost ~5 us of
+    // tail; the stream's counter is left untouched, i.e. zero)
     run_bufs<kGenWaves>(gv, ka, lds, uniform_u64(B0), uniform_u64(B1));
-  } else {
-    run_general<kGenWaves>(g, ka, lds);
+    return;
   }
+  run_general<kGenWaves>(g, ka, lds);
   NVL_FSTAMP(2);
   const Rec* lr = reinterpret_cast<const Rec*>(lds + kRecOff);
   Rec* edge = reinterpret_cast<Rec*>(lds + kEdgeOff);

@@ -46,22 +46,12 @@ constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWave * kWavesPerWG;  // 1024
 constexpr uint32_t kChunk = 4096;
 constexpr uint32_t kUnitsPerWG = 64;  // work units per workgroup (scheduler B)
-// Overhang (tuning knob, off): a buffer's first chunk may hold up to kOver
-// bytes more than 4096, checksummed as a 16-byte piece beside the chunk's 64
-// pieces (a 4097-byte block|type CRC, table/format.cc:90-92, then is ONE
-// pass).  Off, such a buffer is a 1-byte head (crc32c_head_kernel, P = 1
-// lane) plus one full body chunk, which keeps the body kernels' chunk pass
-// free of the overhang's registers and extra lookups.
-#ifndef NVL_OVER
-#define NVL_OVER 0
-#endif
-constexpr uint32_t kOver = NVL_OVER;
-static_assert(kOver == 0 || kOver == 16, "the overhang piece is 16 bytes");
-
 // Chunks of a buffer of L bytes: END-aligned 4096-byte chunks, the first one
-// 1..4096+kOver bytes long (tests/kernel_model.py chunks_of).
+// 1..4096 bytes long (tests/kernel_model.py chunks_of).  (Round 1 tried an
+// overhang -- a first chunk of up to 4096+16 bytes as one pass -- and dropped
+// it: its registers slowed every body pass more than it saved.)
 __host__ __device__ __forceinline__ uint32_t chunks_for(uint64_t L) {
-  return L <= kChunk + kOver ? 1u : (uint32_t)((L - kOver + kChunk - 1) / kChunk);
+  return L <= kChunk ? 1u : (uint32_t)((L + kChunk - 1) / kChunk);
 }
 
 // LDS image (bytes)
@@ -369,6 +359,10 @@ struct FixedGeom {
   const uint32_t* init;
   uint32_t init_all;
   __device__ __forceinline__ uint64_t total() const { return n * (uint64_t)J; }
+  // long_heads' raw metadata (offset from base_addr(), length) of buffer i
+  __device__ __forceinline__ uint64_t offsets_at(uint64_t i) const { return i * stride; }
+  __device__ __forceinline__ uint64_t lengths_at(uint64_t) const { return len; }
+  __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   template <bool F = false>
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
     if constexpr (F) i = udiv_u(t, J);
@@ -407,6 +401,9 @@ struct VarGeom {
   const uint32_t* init;
   uint32_t init_all;
   __device__ __forceinline__ uint64_t total() const { return ldc(chunk_start, n); }
+  __device__ __forceinline__ uint64_t offsets_at(uint64_t i) const { return offsets[i]; }
+  __device__ __forceinline__ uint64_t lengths_at(uint64_t i) const { return lengths[i]; }
+  __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
     uint64_t lo = 0, hi = n;  // invariant: chunk_start[lo] <= t < chunk_start[hi]
     while (hi - lo > 1) {
@@ -446,6 +443,11 @@ struct VarGeom {
 // runs them, so the body kernels' registers never hold masking code.
 enum LoadMode : int { kAligned = 0, kGeneral = 1 };
 
+// Bytes of a buffer's first chunk (END-aligned chunks: the only short one).
+__host__ __device__ __forceinline__ uint32_t head_bytes(uint64_t L, uint32_t J) {
+  return (uint32_t)(L - (uint64_t)kChunk * (J - 1u));
+}
+
 // A buffer's first chunk is a head chunk when it starts before the buffer
 // (partial: 1..4095 bytes) or the buffer is shorter than 4 bytes (bytewise).
 __host__ __device__ __forceinline__ bool head_first(uint64_t L) {
@@ -479,6 +481,45 @@ __device__ __forceinline__ uint32_t lane_load_off(int lane) {
   return ((uint32_t)(lane & 15) << 6) | ((uint32_t)(lane >> 4) << 4);
 }
 
+// kGeneral chunk loads, chunk [cs, ce) with cs = ce - 4096: four row loads
+// and the edge granule.
+//   body chunk (hd false: cs >= p): rows from A4 = cs rounded down to 4 B
+//     (gfx950 serves 4-B aligned dwordx4 at the 16-B aligned rate,
+//     byte-misaligned at ~2/3: tools/diag/ldpat.hip); A4 >= floor4(p) >= g.
+//   head chunk (hd: crc32c_head_kernel's long heads, cs < p): rows from A4
+//     as well; a row slot wholly below p's granule g is loaded from g instead
+//     (its bytes precede the buffer and are masked).  The slot straddling g
+//     reads up to 12 bytes below g: the caller guarantees g is not the first
+//     granule of a 4 KiB page, so they are in g's page (mapped).
+// The edge load is the dword holding byte ce - 1 (lane 63's dword past its
+// row data when the body rows start below cs).  Fault safety: only 16-B
+// granules that hold buffer bytes are touched (tests/kernel_model.py).  The
+// same five loads either way, and no branch around them, so the wait counts
+// stay exact.
+__device__ __forceinline__ void load_general(uintptr_t ce, bool hd, uintptr_t p, int lane, Chunk& ch) {
+  const uintptr_t cs = ce - kChunk;
+  const uint32_t lo = lane_load_off(lane);
+  uintptr_t a[4];
+  if (hd) {
+    const uintptr_t A4 = cs & ~(uintptr_t)3, g = p & ~(uintptr_t)15;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uintptr_t x = A4 + 1024u * (uint32_t)j + lo;
+      a[j] = x + 16u <= g ? g : x;
+    }
+  } else {
+    const uintptr_t A4 = cs & ~(uintptr_t)3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = A4 + 1024u * (uint32_t)j + lo;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const u32x4 v = ld16(a[j]);
+    ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
+  }
+  ch.e[3] = *(const __attribute__((address_space(1))) uint32_t*)((ce - 1u) & ~(uintptr_t)3);
+}
+
 template <int M>
 __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int lane, Chunk& ch) {
   const uintptr_t ce = chunk_end(bi, c);
@@ -505,38 +546,7 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
       ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
     }
   } else {
-    // Four 1 KiB loads from A4, the 4-byte aligned address at or below the
-    // chunk start, plus the edge load (see Chunk).  Fault safety: only 16-B
-    // granules that hold buffer bytes are touched (asserted by
-    // tests/kernel_model.py).  kGeneral chunks start at or after the buffer
-    // start, so A4 >= floor4(p) >= p's granule g.
-    const uint32_t r = (uint32_t)(ce & 3u);
-    const uintptr_t A4 = ce - kChunk - r;
-    const uintptr_t g = (uintptr_t)bi.p & ~(uintptr_t)15;  // granule of the buffer start
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
-      ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
-    }
-    // Edge load: lane 63 when the realign needs the dword past the last
-    // piece (r != 0; the 16 bytes end in the chunk's last dword, which holds
-    // byte ce-1), lane 0 when the chunk has an overhang (chunk 0 starting
-    // after p: the 16 bytes below A4, clamped up to p's granule; build_words
-    // moves them into place).
-    if constexpr (kOver == 0) {
-      // r != 0: the dword past the last piece (it holds byte ce-1); r == 0:
-      // the chunk's last dword (unused).  Every lane loads it (one line, no
-      // branch around the load: the wait counts stay exact).
-      (void)g;
-      ch.e[3] = *(const __attribute__((address_space(1))) uint32_t*)(A4 + (r ? kChunk : kChunk - 4u));
-    } else {
-      const bool ovh = c == 0 && A4 + r > (uintptr_t)bi.p;
-      if ((lane == 63 && r != 0) || (lane == 0 && ovh)) {
-        const uintptr_t ea = lane == 63 ? A4 + kChunk - 12u : (A4 - 16u > g ? A4 - 16u : g);
-        const u32x4 v = ld16(ea);
-        ch.e[0] = v.x; ch.e[1] = v.y; ch.e[2] = v.z; ch.e[3] = v.w;
-      }
-    }
+    load_general(ce, false, (uintptr_t)bi.p, lane, ch);
   }
 }
 
@@ -561,6 +571,10 @@ __device__ __forceinline__ void row_transpose(uint32_t (&d)[16]) {
 __device__ __forceinline__ uint32_t next_lane(uint32_t v, uint32_t last) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)v, 0x130, 0xF, 0xF, false);
 }
+// Previous lane's dword (DPP wave_shr:1); lane 0 gets 0.
+__device__ __forceinline__ uint32_t prev_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
 
 // Zero the bytes of a piece before the buffer start and XOR ~init (s) into the
 // 4 bytes at it: rel = bytes of the piece before the start.  Words below
@@ -584,6 +598,65 @@ __device__ __forceinline__ void mask_inject(uint32_t (&w)[NW], int rel, uint32_t
   }
 }
 
+// Head chunk masking: rel = p - cs bytes of the chunk precede the buffer
+// (wave-uniform, 1 <= rel < 4096 - 1024), i.e. piece lp = rel / 64 holds the
+// buffer start at its word kp, byte bp.  Lanes below lp and lp's words before
+// kp are zeroed (leading zeros leave a zero register unchanged), word kp keeps
+// its bytes from p on and takes ~init << 8bp, the next word ~init's rest.
+// The two words at the uniform index kp are read and written through a
+// vector with a uniform dynamic index (v_movrels / v_movreld): per-word
+// uniform branches cost ~25 % of a long-head pass, and a switch whose cases
+// rewrite many words made the compiler copy the whole array at every join.
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ void head_fix(uint32_t (&w)[16], uint32_t rel, uint32_t s, int lane) {
+  const uint32_t lp = rel >> 6, kp = (rel >> 2) & 15u, bp = rel & 3u;
+  const bool me = (uint32_t)lane == lp;
+  const bool below = (uint32_t)lane < lp;
+  const uint32_t pm = ~0u << (8u * bp), lo = s << (8u * bp), hi = bp ? s >> (32u - 8u * bp) : 0u;
+  u32x16 v;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = (below || (me && (uint32_t)k < kp)) ? 0u : w[k];
+  const uint32_t x = v[kp];
+  v[kp] = me ? ((x & pm) ^ lo) : x;
+  const uint32_t k1 = kp < 15u ? kp + 1u : 0u;  // kp == 15: ~init's rest goes to lane lp + 1's word 0
+  const bool me1 = kp < 15u ? me : (uint32_t)lane == lp + 1u;
+  const uint32_t y = v[k1];
+  v[k1] = me1 ? y ^ hi : y;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = v[k];
+}
+
+// kGeneral words after the transpose (see load_general): lane P holds the 64
+// bytes from the row base + 64P.
+//   shift left by r = cs & 3 bytes (lane P's bytes continue in lane P+1,
+//   lane 63's in the edge dword); then
+//   body chunk: ~init goes into lane 0's first word when the chunk starts
+//     0..3 bytes after the buffer start (a short head holds those bytes);
+//   head chunk: head_fix.
+__device__ __forceinline__ void realign_general(uintptr_t ce, bool hd, uintptr_t p, uint32_t s, int lane,
+                                                const Chunk& ch, uint32_t (&w)[16]) {
+  const uintptr_t cs = ce - kChunk;
+#if !defined(NVL_ABL_NOREALIGN)
+  // (Unconditional -- alignbyte by 0 keeps the low word -- spares the
+  // compiler's register copies at the join but measured slower: scheduler C
+  // 10^5 x 4097 B 85.5 -> 91.5 us, config 3 223 -> 235 us, same box.)
+  const uint32_t r = (uint32_t)(cs & 3u);
+  if (r != 0) {
+    const uint32_t nx = next_lane(w[0], ch.e[3]);
+#pragma unroll
+    for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+    w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
+  }
+#endif
+  if (!hd) {
+    if (cs < p + 4 && lane == 0) w[0] ^= s >> (8u * (uint32_t)(cs - p));
+  } else {
+#if !defined(NVL_ABL_HEADFIX)
+    head_fix(w, (uint32_t)(p - cs), s, lane);
+#endif
+  }
+}
+
 // The lane's 16 words of piece P = lane (64 contiguous bytes), with the ~init
 // injection.
 template <int M>
@@ -597,57 +670,8 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
   if constexpr (M == kAligned) {
     if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0, word 0
   } else {
-    const uintptr_t ce = chunk_end(bi, c);
-    const uintptr_t cs = ce - kChunk;
-    const uintptr_t p = (uintptr_t)bi.p;
-    // Shift the pieces left by r = ce & 3 bytes (the loads started at the
-    // 4-byte aligned address below the chunk start); lane P's bytes continue
-    // in lane P+1 and, for lane 63, in its edge dword e[3].
-    const uint32_t r = (uint32_t)(ce & 3u);
-    if (kOver > 0 && c == 0 && cs > p) {
-      // Overhang: lane 0 turns the o = cs - p bytes before the chunk into a
-      // 16-byte piece ending at cs (bytes before p masked, ~init injected)
-      // from its edge load e[] = the 16 bytes below A4 (clamped up to p's
-      // granule g: moved up by qq dwords) and its first loaded dword (w[0]
-      // before the realign).  chain_fold_ov runs the four words as a chain of
-      // their own; every other lane holds zeros (a zero register stays zero).
-      const uintptr_t A4 = cs - r;
-      const uintptr_t g = p & ~(uintptr_t)15;
-      const uint32_t qq = A4 - 16u >= g ? 0u : (uint32_t)(g - (A4 - 16u)) >> 2;
-      uint32_t D[5];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t v = 0u;
-#pragma unroll
-        for (int m = 0; m <= k; ++m) v = (uint32_t)(k - m) == qq ? ch.e[m] : v;
-        D[k] = v;
-      }
-      D[4] = w[0];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ov[k] = __builtin_amdgcn_alignbyte(D[k + 1], D[k], r);
-      mask_inject<4>(ov, (int)(int64_t)(p - (cs - 16u)), bi.s);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ov[k] = lane == 0 ? ov[k] : 0u;
-    }
-#if !defined(NVL_ABL_NOREALIGN)
-    // (Unconditional -- alignbyte by 0 keeps the low word -- spares the
-    // compiler's register copies at the join but measured slower: scheduler C
-    // 10^5 x 4097 B 85.5 -> 91.5 us, config 3 223 -> 235 us, same box.)
-    if (r != 0) {
-      // lane 63's dword past the last piece: its edge load's e[3]
-      const uint32_t nx = next_lane(w[0], ch.e[3]);
-#pragma unroll
-      for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
-      w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
-    }
-#endif
-    if (cs < p + 4) {
-      // a chunk that starts at the buffer start, or 1..3 bytes after it (a
-      // head or the overhang holds those bytes): ~init, or what of it reaches
-      // past them, goes into lane 0's first word (body chunks start at or
-      // after p)
-      if (lane == 0) w[0] ^= bi.s >> (8u * (uint32_t)(cs - p));
-    }
+    (void)ov;
+    realign_general(chunk_end(bi, c), false, (uintptr_t)bi.p, bi.s, lane, ch, w);
   }
 }
 
@@ -735,32 +759,6 @@ __device__ __forceinline__ uint32_t chain_fold(const uint8_t* lds, const LaneBas
   for (int k = 0; k < 16; ++k) w1[0][k] = w[k];
   chains<1, false>(lds, lb, w1, lane, r);
   return r[0];
-}
-
-// The same for a first chunk with an overhang piece ov (16 bytes before the
-// chunk; nonzero in lane 0 only, see build_words): its raw register runs as a
-// second, independent 4-step chain beside the main one and joins lane 0's
-// chain shifted by that lane's 64-byte piece (comb table 0), so the serial
-// path stays 16 steps + butterfly (as one prepended 20-step chain it was 25 %
-// longer: 4097-byte buffers ran 115 us vs 91 us for 4096-byte ones).
-__device__ __forceinline__ uint32_t chain_fold_ov(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[16],
-                                                  const uint32_t (&ov)[4], int lane) {
-  uint32_t crc = w[0], a = ov[0];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    crc = slice4_next(lds, crc, k < 15 ? w[k + 1] : 0u, lb);
-    if (k < 4) a = slice4_next(lds, a, k < 3 ? ov[k + 1] : 0u, lb);
-  }
-  const uint8_t* c0 = lds + kCombOff;  // comb level 0: shift by 64 bytes, byte j in sub-table j
-  crc ^= xor3(lds_u32(c0, (a & 0xFFu) << 2), lds_u32(c0 + 1024u, ((a >> 8) & 0xFFu) << 2),
-              lds_u32(c0 + 2048u, ((a >> 16) & 0xFFu) << 2)) ^
-         lds_u32(c0 + 3072u, (a >> 24) << 2);
-  crc = fold_level<0, 0, false>(lds, crc, lane);
-  crc = fold_level<1, 1, false>(lds, crc, lane);
-  crc = fold_level<2, 2, false>(lds, crc, lane);
-  crc = fold_level<3, 3, false>(lds, crc, lane);
-  crc = fold_level<4, 4, false>(lds, crc, lane);
-  return fold_level<5, 5, false>(lds, crc, lane);
 }
 
 template <int M>
@@ -1074,13 +1072,9 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
     if (q1v) load_chunk<M>(q1.bi, q1.c, lane, n1);
     if (work) {
       NVL_COUNT();
-      // a first chunk with an overhang: lane 0's piece starts 16 bytes early
-      const bool ovh = kOver > 0 && M == kGeneral && p0.c == 0 && chunk_end(p0.bi, 0) - kChunk > (uintptr_t)p0.bi.p;
       uint32_t r[2];
       if (two) {
         chains<2, false>(lds, lb, w, lane, r);
-      } else if (ovh) {
-        r[0] = chain_fold_ov(lds, lb, w[0], ov[0], lane);
       } else {
         r[0] = chain_fold<M>(lds, lb, w[0], lane);
       }
@@ -1116,163 +1110,9 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   NVL_STAMP_END();
 }
 
-// ---------------------------------------------------------------------------
-// Scheduler B, pipelined (kGeneral; NVL_GEN_PP): the same work units and
-// records as run_units, with two chunk buffers A and B in ping-pong.  A
-// generator walks the chunk stream (pulling units from the LDS counter as it
-// goes); each buffer is refilled from it right after its words are built, so
-// a chunk's loads have two chunk passes to arrive instead of one (with one in
-// flight per wave the waves waited on memory ~half their cycles: general
-// chunks ran at 4.6 TB/s, aligned pairs at 6.3).  Every refill issues the
-// same loads whatever the chunk (a head chunk, or past the end of the work:
-// reads of the table blob, unused), so the compiler's wait counts at the loop
-// head keep the other buffer in flight.
-struct ChunkP {
-  uint32_t d[16];
-  uint32_t e;   // the dword at A4 + 4096 (lane 63's realign word)
-  uint32_t hv;  // hc[i] when this is the buffer's first body chunk (see hv_used)
-};
-
-struct Slot {  // wave-uniform: what a buffer holds
-  Pos pos;
-  uint32_t u;
-  bool valid, start, end, work;
-};
-
-__device__ __forceinline__ void load_chunk_pp(const Slot& s, int lane, uintptr_t safe, const uint32_t* hc,
-                                              ChunkP& ch) {
-  const uintptr_t ce = chunk_end(s.pos.bi, s.pos.c);
-  const uint32_t r = (uint32_t)(ce & 3u);
-  const uintptr_t A4 = s.work ? ce - kChunk - r : safe;
-  const uint32_t lo = lane_load_off(lane);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const u32x4 v = ld16(A4 + 1024u * (uint32_t)j + lo);
-    ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
-  }
-  // r != 0: the dword past the chunk's last piece (holds byte ce-1); r == 0:
-  // the chunk's last dword (unused) -- every lane loads it, one line
-  ch.e = *(const __attribute__((address_space(1))) uint32_t*)(A4 + (r ? kChunk : kChunk - 4u));
-  const uintptr_t ha = hc && s.work ? (uintptr_t)(hc + s.pos.i) : safe;
-  ch.hv = __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)ha);
-}
-
-template <int NW, class G>
-__device__ __forceinline__ void run_units_pp(const G& g, const KArgs& ka, uint8_t* lds) {
-  static_assert(kOver == 0, "the pipelined loop has no overhang piece");
-  NVL_STAMP0();
-  const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t T = g.total();
-  const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
-  const uintptr_t safe = (uintptr_t)ka.tables;  // >= 4100 valid bytes
-  auto lo_of = [&](uint32_t uu) -> uint64_t { return g.template unit_lo<true>(T, uu); };
-  auto first_body = [&](const Pos& q) -> uint32_t { return head_first(q.bi.len) ? 1u : 0u; };
-  const Rec none{kNoBuf, 0u, 0u};
-
-  // generator: the unit being walked, its next chunk, its end
-  uint32_t gu = ub0 + wv;
-  uint64_t gt = lo_of(gu), gt1 = lo_of(gu + 1);
-  bool fresh = true, done = false, synced = false;
-  Pos last{};
-  auto gen = [&](Slot& sl) {
-    sl.valid = false;
-    sl.work = false;
-    while (!done && gt >= gt1) {  // unit exhausted (or empty): the next one
-      if (!synced) return;        // (no pulls before the workgroup barrier)
-      gu = ub0 + pull_unit(lds, lane);
-      if (gu >= ub1) {
-        done = true;
-        return;
-      }
-      gt = lo_of(gu);
-      gt1 = lo_of(gu + 1);
-      fresh = true;
-      if (gt >= gt1 && lane == 0) g.put_recs(ka, lds, gu, none, none);  // an empty unit
-    }
-    if (done) return;
-    sl.valid = true;
-    sl.u = gu;
-    sl.start = fresh;
-    sl.end = gt + 1 == gt1;
-    sl.pos = fresh ? unit_start_pos<true>(g, gu, gt) : next_pos(g, last);
-    sl.work = !(sl.pos.c == 0 && head_first(sl.pos.bi.len));
-    last = sl.pos;
-    fresh = sl.end;
-    ++gt;
-  };
-  auto hv_used = [&](const Slot& sl) -> bool { return ka.hc && sl.pos.c == 1u && head_first(sl.pos.bi.len); };
-
-  Slot sA, sB;
-  ChunkP cA, cB;
-  if (gt >= gt1 && lane == 0) g.put_recs(ka, lds, gu, none, none);  // the pre-assigned unit is empty
-  gen(sA);  // the first two chunks of the pre-assigned unit load during the LDS fill
-  load_chunk_pp(sA, lane, safe, ka.hc, cA);
-  asm volatile("" ::: "memory");
-  gen(sB);
-  load_chunk_pp(sB, lane, safe, ka.hc, cB);
-  fill_lds<NW>(lds, ka.tables);
-  __syncthreads();
-  synced = true;
-  const LaneBase lb = make_lane_base(lane);
-  NVL_STAMP1();
-
-  UnitState st{0u, 0u, true, none};
-  Rec tail = none;
-  // One buffer: build its words (the buffer dies), refill it from the
-  // generator, then run the chains and the unit bookkeeping.
-  auto step = [&](Slot& sl, ChunkP& ch) {
-    if (!sl.valid) {  // (only B right after the barrier: its unit had one chunk)
-      gen(sl);
-      load_chunk_pp(sl, lane, safe, ka.hc, ch);
-      return;
-    }
-    if (sl.start) {
-      st = UnitState{0u, 0u, sl.pos.c <= first_body(sl.pos), none};
-      tail = none;
-    }
-    const Slot cur = sl;
-    uint32_t w[16], ov[4];
-    const uint32_t hx = hv_used(cur) ? ch.hv : 0u;
-    if (cur.work) {
-      Chunk c1;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) c1.d[k] = ch.d[k];
-      c1.e[3] = ch.e;
-      build_words<kGeneral>(cur.pos.bi, cur.pos.c, lane, c1, w, ov);
-    }
-    gen(sl);
-    load_chunk_pp(sl, lane, safe, ka.hc, ch);
-    asm volatile("" ::: "memory");
-    if (cur.work) {
-      NVL_COUNT();
-      const uint32_t r = chain_fold<kGeneral>(lds, lb, w, lane);
-      consume(st, cur.pos, r, lds, lane, ka, hx);
-    }
-    if (cur.end) {
-      if (st.cnt) {  // the unit ends inside a buffer: its portion, normalized to the buffer end
-        const uint32_t norm = normalize(lds, ka.tables, st.acc, cur.pos.bi.J - 1u - cur.pos.c, lane);
-        if (st.from_zero) tail = Rec{cur.pos.i, norm, st.cnt};
-        else st.head = Rec{cur.pos.i, norm, st.cnt};
-      }
-      if (lane == 0) g.put_recs(ka, lds, cur.u, st.head, tail);
-    }
-  };
-  while (true) {  // (an invalid slot past the end loads the table blob and does nothing)
-    step(sA, cA);
-    step(sB, cB);
-    if (done && !sA.valid && !sB.valid) break;
-  }
-  NVL_STAMP_END();
-}
-
-#ifndef NVL_GEN_PP
-#define NVL_GEN_PP 0  // kGeneral chunks: 1 = run_units_pp (two chunks in flight per wave; measured no faster, more SGPR spills), 0 = run_units
-#endif
 template <int NW, class G>
 __device__ __forceinline__ void run_general(const G& g, const KArgs& ka, uint8_t* lds) {
-  if constexpr (NVL_GEN_PP) run_units_pp<NW>(g, ka, lds);
-  else run_units<kGeneral, NW>(g, ka, lds);
+  run_units<kGeneral, NW>(g, ka, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1722,8 +1562,126 @@ __device__ __forceinline__ uint32_t bitwise_raw(const uint8_t* p, uint32_t n, ui
   return l;
 }
 
+// Head kernel LDS beyond the table image: the long-head list of a sub-range
+// (u32 size, u32 drained, u16 index[kHeadSub]).
+constexpr uint64_t kHeadSub = (uint64_t)kWave * kWavesPerWG;  // buffers per sub-range: <= 64 per wave
+constexpr uint32_t kLongOff = kLdsBytes;
+constexpr uint32_t kHeadLdsBytes = kLongOff + 8u + 2u * (uint32_t)kHeadSub;
+static_assert(kLongOff % 16u == 0u && kHeadLdsBytes <= 160u * 1024u, "head kernel LDS exceeds 160 KiB");
+constexpr uint32_t kLongOk = 1u << 16, kLongLast = 1u << 17;  // long-head tags: index within the sub-range | flags
+
+// Long heads of a sub-range (its LDS list), two per pass with interleaved
+// chains, pulled from the list by every wave of the workgroup.  A head is a
+// whole chunk [ce - 4096, ce) with its bytes before p masked (load_general /
+// realign_general with hd).  Pipeline: a pass builds the words of the pair in
+// hand (waiting for their loads), turns the next pair's metadata -- loaded a
+// pass earlier, before those chunk loads -- into positions, pulls the pair
+// after it and issues its metadata loads, issues the next pair's chunk loads,
+// then runs the chains.  Past the end of the list a slot is a dummy chunk in
+// the table blob (loaded, not written).
+template <class G>
+__device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t* lds, const LaneBase& lb,
+                                           uint64_t sub0, uint32_t* lcnt, const uint16_t* llist) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nl = (uint32_t)__builtin_amdgcn_readfirstlane((int)lcnt[0]);
+  if (nl == 0) return;
+  const uintptr_t safe = (uintptr_t)ka.tables;
+  const uint32_t* const ibase = g.init ? g.init : reinterpret_cast<const uint32_t*>(safe);
+  auto pull = [&]() -> uint32_t {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(&lcnt[1], 2u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+  };
+  // metadata of list entries k, k+1 (raw loads; all lanes the same address)
+  uint32_t k = pull();
+  uint64_t mo0, mL0, mo1, mL1;
+  uint32_t mi0, mi1, mj0, mj1;
+#define NVL_META(K)                                                                                    \
+  do {                                                                                                 \
+    mj0 = (K) < nl ? (uint32_t)llist[(K)] | kLongOk : 0u;                                              \
+    mj1 = (K) + 1u < nl ? (uint32_t)llist[(K) + 1u] | kLongOk : 0u;                                    \
+    const uint64_t i0_ = sub0 + (mj0 & 0xFFFFu), i1_ = sub0 + (mj1 & 0xFFFFu);                         \
+    mo0 = g.offsets_at(i0_);                                                                           \
+    mL0 = g.lengths_at(i0_);                                                                           \
+    mi0 = ibase[g.init ? i0_ : 0u];                                                                    \
+    mo1 = g.offsets_at(i1_);                                                                           \
+    mL1 = g.lengths_at(i1_);                                                                           \
+    mi1 = ibase[g.init ? i1_ : 0u];                                                                    \
+  } while (0)
+  // a position from loaded metadata (uniform: lane 0's copy)
+#define NVL_POS(MO, ML, MI, MJ, CE, P, S, TAG)                                                          \
+  do {                                                                                                 \
+    TAG = (uint32_t)__builtin_amdgcn_readfirstlane((int)(MJ));                                          \
+    const uint64_t L_ = uniform_u64(ML);                                                               \
+    const uint32_t J_ = chunks_for(L_);                                                                \
+    P = (TAG & kLongOk) ? g.base_addr() + uniform_u64(MO) : safe + 16u;                                 \
+    CE = (TAG & kLongOk) ? P + head_bytes(L_, J_) : safe + kChunk;                                     \
+    S = ~(g.init ? uniform_u32(MI) : g.init_all);                                                      \
+    TAG |= (J_ == 1u) ? kLongLast : 0u;                                                                \
+  } while (0)
+#define NVL_WRITE(TAG, RAW)                                                                            \
+  do {                                                                                                 \
+    if (((TAG) & kLongOk) && lane == 0) {                                                              \
+      const uint64_t ib_ = sub0 + ((TAG) & 0xFFFFu);                                                   \
+      if ((TAG) & kLongLast) ka.out[ib_] = finish(~(RAW), ka.flags);                                   \
+      else ka.hc[ib_] = (RAW);                                                                         \
+    }                                                                                                  \
+  } while (0)
+  NVL_META(k);
+  uintptr_t ceA, pA, ceB, pB;
+  uint32_t sA, tA, sB, tB;
+  NVL_POS(mo0, mL0, mi0, mj0, ceA, pA, sA, tA);
+  NVL_POS(mo1, mL1, mi1, mj1, ceB, pB, sB, tB);
+  k = pull();
+  NVL_META(k);
+  Chunk cA, cB;
+  load_general(ceA, true, pA, lane, cA);
+  load_general(ceB, true, pB, lane, cB);
+  while (true) {
+    uint32_t w[2][16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[0][q] = cA.d[q];
+    row_transpose(w[0]);
+    realign_general(ceA, true, pA, sA, lane, cA, w[0]);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[1][q] = cB.d[q];
+    row_transpose(w[1]);
+    realign_general(ceB, true, pB, sB, lane, cB, w[1]);
+    const uint32_t uA = tA, uB = tB;
+    NVL_POS(mo0, mL0, mi0, mj0, ceA, pA, sA, tA);
+    NVL_POS(mo1, mL1, mi1, mj1, ceB, pB, sB, tB);
+    k = pull();
+    NVL_META(k);
+    load_general(ceA, true, pA, lane, cA);
+    load_general(ceB, true, pB, lane, cB);
+    uint32_t raws[2];
+#if defined(NVL_ABL_LONGNOCHAIN)
+    raws[0] = w[0][0] ^ w[0][15];
+    raws[1] = w[1][0] ^ w[1][15];
+#else
+    chains<2, false>(lds, lb, w, lane, raws);
+#endif
+    NVL_WRITE(uA, raws[0]);
+    NVL_WRITE(uB, raws[1]);
+    if (!(uB & kLongOk)) break;  // (entries are drained in order per wave: uA empty implies uB empty)
+  }
+#undef NVL_WRITE
+#undef NVL_POS
+#undef NVL_META
+}
+
+#if defined(NVL_DIAG_HSTAMPS)
+// Diagnostic build only: per-wave {start, tables ready, end, long-head cycles}
+// of the head kernel (s_memrealtime), read back with nvl_diag_hstamps().
+__device__ unsigned long long g_hstamps[4 * 65536];
+#endif
+
 template <class G>
 __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* lds) {
+#if defined(NVL_DIAG_HSTAMPS)
+  const unsigned long long hs0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long hs_long = 0;
+#endif
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the workgroup's buffers: its plan tile when there is one
@@ -1736,20 +1694,43 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       w1 = min(g.n, w0 + ka.tile_S);
     }
   }
-  const uint64_t b0 = w0 + (w1 - w0) * wv / kWavesPerWG, b1 = w0 + (w1 - w0) * (wv + 1) / kWavesPerWG;
+  // The workgroup's buffers go in sub-ranges of kHeadSub, a slice of at most
+  // 64 buffers (one per lane) per wave.  Short heads run in the wave's own lane-group rounds; long
+  // heads are appended to an LDS list that all waves then drain two at a
+  // time (long_heads): with a static per-wave split the waves' long-head
+  // time ranged 36..96 us for equal work (issue arbitration favours older
+  // waves; tools/diag/hstamps.py).
   const LaneBase lb = make_lane_base(lane);
+  uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds + kLongOff);  // [0] list size, [1] drained
+  uint16_t* llist = reinterpret_cast<uint16_t*>(lds + kLongOff + 8u);
   uintptr_t lp = 0;  // the lane's buffer of the current group: start, length, ~init
   uint64_t lL = 0;
   uint32_t ls = 0;
-  if (b0 + (uint64_t)lane < b1) g.lane_meta(b0 + (uint64_t)lane, lp, lL, ls);  // in flight during the fill
+  // the wave's slice of a sub-range [s0, s1): at most 64 buffers
+  auto slice = [&](uint64_t s0, uint64_t s1, uint64_t& a, uint64_t& b) {
+    a = s0 + (s1 - s0) * wv / kWavesPerWG;
+    b = s0 + (s1 - s0) * (wv + 1) / kWavesPerWG;
+  };
+  {
+    uint64_t a, b;
+    slice(w0, min(w1, w0 + kHeadSub), a, b);
+    if (a + (uint64_t)lane < b) g.lane_meta(a + (uint64_t)lane, lp, lL, ls);  // in flight during the fill
+  }
+  if (threadIdx.x < 2) lcnt[threadIdx.x] = 0u;
   if (tables) {
     fill_lds<kWavesPerWG>(lds, ka.tables);
     __syncthreads();
   }
-  for (uint64_t gb = b0; gb < b1; gb += kWave) {
-    const bool valid = gb + (uint64_t)lane < b1;
+#if defined(NVL_DIAG_HSTAMPS)
+  const unsigned long long hs1 = __builtin_amdgcn_s_memrealtime();
+#endif
+  for (uint64_t sub0 = w0; sub0 < w1; sub0 += kHeadSub) {  // (workgroup-uniform trip count)
+    const uint64_t sub1 = min(w1, sub0 + kHeadSub);
+    uint64_t gb, ge;
+    slice(sub0, sub1, gb, ge);
+    const bool valid = gb + (uint64_t)lane < ge;
     const uint64_t i = gb + (uint64_t)lane;
-    if (gb != b0) {
+    if (sub0 != w0) {
       lp = 0;
       lL = 0;
       ls = 0;
@@ -1767,11 +1748,28 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     // hc = raw(0, head ^ s's low bytes) = raw(s, head) ^ (s >> 8 hl): the body
     // injects s's remaining bytes into its first word itself
     if (shrt) ka.hc[i] = bitwise_raw(reinterpret_cast<const uint8_t*>(lp), (uint32_t)hl, ls) ^ (ls >> (8u * (uint32_t)hl));
+    // Long heads (1025..4095 bytes) run as whole chunks with the body
+    // kernels' coalesced row loads and transpose (long_heads): as P = 64
+    // lane-group rounds, whose 64-byte-per-lane loads touch 32 lines per
+    // instruction, this class ran at ~2.7 TB/s.  A head whose buffer starts
+    // in the first 16 bytes of a 4 KiB page stays in the rounds (load_general
+    // reads up to 12 bytes below p's granule).
+    const bool coal = head && cls == 3u && ((lp >> 4) & 255u) != 0u;  // (load_general: g not a page start)
+    {
+      const uint64_t mco = __ballot(coal);
+      if (mco) {  // append to the workgroup's list (index within the sub-range)
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&lcnt[0], (uint32_t)__builtin_popcountll(mco));
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mco >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mco, 0u));
+        if (coal) llist[base + rank] = (uint16_t)(i - sub0);
+      }
+    }
     uint64_t m[4];
     uint32_t nr[4], NR = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      m[c] = __ballot(head && cls == (uint32_t)c);
+      m[c] = __ballot(head && !coal && cls == (uint32_t)c);
       const uint32_t per = 64u >> (2 * c);
       nr[c] = ((uint32_t)__builtin_popcountll(m[c]) + per - 1u) / per;
       NR += nr[c];
@@ -1802,7 +1800,7 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       h.hl = hx & 0xFFFFu;
       h.tag = src | (ok ? kHeadOk : 0u) | (hx >> 16);
     };
-    if (NR == 0) continue;
+    if (NR != 0) {
     // Two buffers, A and B, in ping-pong: a buffer's next round is loaded
     // right after its words are built (the registers carry over, no copies),
     // so each round's loads have two rounds of chains to arrive.  Past the
@@ -1849,12 +1847,37 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       finish_round(head_chain(lds, lb, w, nl, lane), tag, P);
     }
     // (the last reloads drain before the next group's buffers are set up)
+    }
+    if (tables) {  // (workgroup-uniform)
+      __syncthreads();  // the list is complete
+#if defined(NVL_DIAG_HSTAMPS)
+      const unsigned long long hl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+      long_heads(g, ka, lds, lb, sub0, lcnt, llist);
+#if defined(NVL_DIAG_HSTAMPS)
+      hs_long += __builtin_amdgcn_s_memrealtime() - hl0;
+#endif
+      __syncthreads();  // drained
+      if (threadIdx.x < 2) lcnt[threadIdx.x] = 0u;
+      __syncthreads();
+    }
   }
+#if defined(NVL_DIAG_HSTAMPS)
+  {
+    const uint32_t wave_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0 && wave_ < 65536) {
+      g_hstamps[4 * wave_ + 0] = hs0;
+      g_hstamps[4 * wave_ + 1] = hs1;
+      g_hstamps[4 * wave_ + 2] = __builtin_amdgcn_s_memrealtime();
+      g_hstamps[4 * wave_ + 3] = hs_long;
+    }
+  }
+#endif
 }
 
 template <class G>
 __global__ __launch_bounds__(kThreads, 1) void crc32c_head_kernel(G g, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLdsBytes];
   run_heads(g, ka, lds);
 }
 
@@ -2538,6 +2561,11 @@ size_t var_unit_map_bytes(int num_cu) { return (uint64_t)num_cu * dev::kUnitsPer
 #if defined(NVL_DIAG_FUSED)
 extern "C" __attribute__((visibility("default"))) int nvl_diag_fstamps(unsigned long long* host, size_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_fstamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
+#if defined(NVL_DIAG_HSTAMPS)
+extern "C" __attribute__((visibility("default"))) int nvl_diag_hstamps(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_hstamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
 }
 #endif
 #if defined(NVL_DIAG_STAMPS)

@@ -99,7 +99,7 @@ def wave_fold(g):
     return g[0]
 
 
-OVER = 0  # overhang (NVL_OVER, off): a first chunk of up to 4096 + OVER bytes is ONE pass
+OVER = 0  # overhang (round-1 knob, removed from the kernels): a first chunk of up to 4096 + OVER bytes is ONE pass
 
 
 def chunks_of(L: int) -> int:
@@ -188,12 +188,63 @@ def head_raw(mem: bytes, p: int, L: int, J: int, s: int) -> int:
     return group_fold(lanes, P.bit_length() - 1)
 
 
+def long_head(p: int, hl: int) -> bool:
+    """crc32c_kernels.hip run_heads: a head of 1025..4095 bytes runs as a whole
+    chunk (long_heads) unless the buffer starts in the first 16 bytes of a
+    4 KiB page."""
+    return 1024 < hl < CHUNK and ((p >> 4) & 255) != 0
+
+
+def long_head_raw(mem: bytes, p: int, L: int, J: int, s: int) -> int:
+    """Raw register of a long head the way long_heads runs it
+    (load_general / realign_general with hd): the chunk [ce - 4096, ce) loaded
+    as 256 16-byte row slots from the 4-byte aligned A4 at or below its start
+    plus the dword holding byte ce - 1; a slot wholly below p's granule g is
+    loaded from g (garbage), the one straddling g reads up to 12 bytes below
+    g, which must lie in g's 4 KiB page; bytes before p zeroed and ~init
+    injected at p (head_fix)."""
+    hl = L - CHUNK * (J - 1)
+    assert long_head(p, hl)
+    ce = p + hl
+    cs = ce - CHUNK
+    g = p & ~15
+    A4 = cs & ~3
+    r = cs & 3
+
+    def load(a: int, n: int) -> bytes:
+        # fault safety: granules up to the one holding ce - 1; below g only
+        # inside g's page
+        assert ((a + n - 1) & ~15) <= ((ce - 1) & ~15), (a, n, p, ce)
+        assert (a & ~15) >= g or (a >> 12) == (g >> 12), (a, n, p, g)
+        return mem[a:a + n]
+
+    data = bytearray(CHUNK + 4)
+    for k in range(CHUNK // 16):
+        a = A4 + 16 * k
+        data[16 * k:16 * k + 16] = load(g if a + 16 <= g else a, 16)
+    data[CHUNK:CHUNK + 4] = load((ce - 1) & ~3, 4)
+    piece = bytearray(data[r:r + CHUNK])  # bytes [cs, ce), garbage before p
+    rel = p - cs
+    piece[:rel] = bytes(rel)
+    for q in range(4):
+        piece[rel + q] ^= (s >> (8 * q)) & 0xFF
+    lanes = []
+    for lane in range(64):
+        crc = 0
+        for k in range(16):
+            crc = slice4(crc ^ int.from_bytes(piece[64 * lane + 4 * k:64 * lane + 4 * k + 4], "little"))
+        lanes.append(crc)
+    return wave_fold(lanes)
+
+
 def chunk_raw(mem: bytes, p: int, L: int, J: int, c: int, s: int) -> int:
     """Raw register of chunk c of buffer [p, p+L) with ~init = s injected,
     computed the way load_chunk<kGeneral> / build_words<kGeneral> do it (a
-    partial first chunk: the head kernel's lane groups, head_raw)."""
+    partial first chunk: the head kernel, long_head_raw or head_raw)."""
     e = p + L
     if c == 0 and e - CHUNK * (J - 1) - CHUNK < p:
+        if L >= 4 and long_head(p, L - CHUNK * (J - 1)):
+            return long_head_raw(mem, p, L, J, s)
         return head_raw(mem, p, L, J, s)
     ce = e - CHUNK * (J - 1 - c)
     cs = ce - CHUNK

@@ -112,13 +112,12 @@ def test_general_path_model(port, seed):
     assert got == want
 
 
-@pytest.mark.parametrize("over", [0, 16])
-def test_overhang_alignment_sweep_model(port, over, monkeypatch):
-    """Every start alignment mod 16 x lengths around the chunk and overhang
-    boundaries (4096, 4096 + OVER) through the model, with garbage before and
-    after each buffer; the model also asserts that no load touches a 16-byte
-    granule without buffer bytes (fault safety)."""
-    monkeypatch.setattr(km, "OVER", over)  # the shipped kernels: NVL_OVER = 0 (a tuning build: 16)
+def test_alignment_sweep_model(port):
+    """Every start alignment mod 16 x lengths around the chunk boundaries
+    through the model, with garbage before and after each buffer; the model
+    also asserts that no load touches a 16-byte granule without buffer bytes
+    (fault safety) -- or, for a long head's straddling row slot, bytes outside
+    its granule's page."""
     mem = bytes(port.fill(0xA11, 0, 200000))
     lens = [4, 5, 6, 7, 15, 16, 17, 63, 64, 65, 255, 256, 257, 1023, 1024, 1025, 4095, 4096, 4097, 4098, 4099,
             4100, 4101, 4108, 4111, 4112, 4113, 4114, 4160, 4161, 4352, 4353, 5120, 5121, 8191, 8207, 8208, 8209,
@@ -133,3 +132,23 @@ def test_overhang_alignment_sweep_model(port, over, monkeypatch):
         got = km.batch(mem, bufs, inits, 1)
         want = [port.extend(i, mem[p:p + L]) for (p, L), i in zip(bufs, inits)]
         assert got == want, a
+
+
+@pytest.mark.parametrize("page_off", [0, 4, 15, 16, 17, 28, 4079, 4080])
+def test_long_head_model(port, page_off):
+    """Long heads (1025..4095 bytes, run_heads -> long_heads) at starts around a
+    4 KiB page boundary: buffers starting in a page's first granule take the
+    lane-group path (head_raw), the rest the whole-chunk path (long_head_raw,
+    whose straddling row slot must stay in its granule's page)."""
+    mem = bytes(port.fill(0x10E6, 0, 64 * 4096))
+    rng = random.Random(page_off)
+    for k in range(40):
+        hl = rng.choice([1025, 1026, 1027, 1028, 1100, 2047, 2048, 2049, 3000, 4000, 4080, 4081, 4092, 4094, 4095])
+        J = rng.choice([1, 1, 2, 3])
+        L = hl + 4096 * (J - 1)
+        p = 4096 * (2 + 13 * k % 40) + page_off
+        s = rng.getrandbits(32)
+        assert km.long_head(p, hl) == (((p >> 4) & 255) != 0)
+        got = km.chunk_raw(mem, p, L, J, 0, s)
+        assert got == km.raw_bytes(0, bytes(4096 - hl) + bytes(b ^ ((s >> (8 * q)) & 0xFF) if q < 4 else b
+                                                              for q, b in enumerate(mem[p:p + hl]))), (p, hl)

@@ -1176,7 +1176,8 @@ __device__ __forceinline__ void build_pos(const CPos& q, int lane, const Chunk& 
 }
 
 template <int NW, class G>
-__device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* lds, uint64_t i0, uint64_t i1) {
+__device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* lds, uint64_t i0, uint64_t i1,
+                                         const uint16_t* perm = nullptr) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1204,10 +1205,12 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   // group's metadata), then adopts groups and issues the next loads: an
   // adoption never waits on a load still in flight.  fill_lds starts the LDS
   // counter at 2 * NW: groups wv and NW + wv are pre-assigned.
-  uint64_t gb = 0, todo = 0;  // todo: group lanes whose buffers have body chunks, not started
+  // perm (LDS, optional): the range's buffers in the order they are handed
+  // out (lpt_order: most chunks first), as indices relative to i0.
+  uint64_t todo = 0;  // todo: group lanes whose buffers have body chunks, not started
   uintptr_t lp = 0;
   uint64_t lL = 0;
-  uint32_t ls = 0;
+  uint32_t ls = 0, lr = 0;  // lr: the lane's buffer - i0
   uint64_t ngb = 0;
   uint32_t ngn = 0;
   bool has_nxt = false, nxt_ready = false;
@@ -1217,7 +1220,7 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   // copy at a control-flow join -- such a copy waits for the load (with
   // conditional loads the compiler waited right after issuing them).
   uint64_t no = 0, nL = 0;
-  uint32_t ni = 0;
+  uint32_t ni = 0, nr = 0;
   auto claim_group = [&](uint64_t k) {  // the next group's index (scalars only)
     has_nxt = k < ngroups;
     nxt_ready = false;
@@ -1226,7 +1229,9 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   };
   const uint32_t* const ibase = g.init ? g.init : reinterpret_cast<const uint32_t*>(safe);
   auto meta_load = [&]() {
-    const uint64_t i = ngb + (uint64_t)min<uint32_t>((uint32_t)lane, ngn - 1u);  // < n (buffer 0 when none)
+    const uint64_t pos = ngb + (uint64_t)min<uint32_t>((uint32_t)lane, ngn - 1u);  // < n (buffer 0 when none)
+    const uint64_t i = perm && pos >= i0 ? i0 + perm[pos - i0] : pos;
+    nr = (uint32_t)(i - i0);
     no = g.offsets[i];
     nL = g.lengths[i];
     ni = ibase[g.init ? i : 0u];
@@ -1235,7 +1240,7 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
     lp = (uintptr_t)g.base + no;
     lL = nL;
     ls = ~(g.init ? ni : g.init_all);
-    gb = ngb;
+    lr = nr;
     todo = __ballot((uint32_t)lane < ngn && chunks_for(lL) > (head_first(lL) ? 1u : 0u));
     has_nxt = false;
   };
@@ -1267,7 +1272,7 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
       cL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lL >> 32), (int)j) << 32) |
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lL, (int)j);
       cx = (uint32_t)__builtin_amdgcn_readlane((int)ls, (int)j);
-      ci = gb + j;
+      ci = i0 + (uint32_t)__builtin_amdgcn_readlane((int)lr, (int)j);
       cJ = chunks_for(cL);
       cfb = head_first(cL) ? 1u : 0u;
       cc = cfb;
@@ -2195,7 +2200,8 @@ static_assert(kTbResOff + 16u <= kSliceOff + kRepBytes, "tiled plan scratch must
 
 template <int NW>
 __device__ __forceinline__ void tiled_plan(uint8_t* lds, const VarGeom& g, const KArgs& ka, uint64_t& C0,
-                                           uint64_t& C1, bool& long_bufs, uint64_t& B0, uint64_t& B1) {
+                                           uint64_t& C1, bool& long_bufs, uint64_t& B0, uint64_t& B1,
+                                           bool& multi) {
   constexpr uint32_t kT = kWave * NW;
   static_assert(kT == 1024, "64 searches of 16 lanes fill the block");
   uint64_t* tb = reinterpret_cast<uint64_t*>(lds);
@@ -2208,6 +2214,7 @@ __device__ __forceinline__ void tiled_plan(uint8_t* lds, const VarGeom& g, const
   const uint64_t tot = t < Gt ? ka.tiles[2ull * t] : 0;
   const uint64_t mj = t < Gt ? ka.tiles[2ull * t + 1] : 0;
   long_bufs = __syncthreads_or(mj > kBufsMaxJ ? 1 : 0) != 0;
+  multi = __syncthreads_or(mj > 2 ? 1 : 0) != 0;
   uint64_t x = tot;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -2305,13 +2312,71 @@ __device__ __forceinline__ Rec load_edge(gu64* g) {
   return Rec{b, (uint32_t)v, (uint32_t)(v >> 32)};
 }
 
+// Longest-processing-time order for scheduler C (fused kernel, whole
+// buffers): the workgroup's buffers by body chunks, most first, so the last
+// groups handed out are the smallest.  In range order the waves of a
+// workgroup finished 26..43 us apart on config 3 (buffers of up to 16
+// chunks, ~4.6 us per two-chunk step: tools/diag/bstamps.py).  A counting
+// sort over the 33 chunk counts in LDS beyond the table image (scheduler B's
+// unit/record area, unused here); nullptr when the range is larger than the
+// permutation space.
+constexpr uint32_t kPermOff = kLdsBytes;             // u32 bucket[33], then u16 perm[kPermMax]
+constexpr uint32_t kPermMax = 1792;  // (the compiler adds ~264 B of its own to this kernel)
+constexpr uint32_t kPermLdsBytes = kPermOff + 136u + 2u * kPermMax;
+static_assert(kPermLdsBytes <= 160u * 1024u, "permutation exceeds LDS");
+
+template <int NW>
+__device__ const uint16_t* lpt_order(const VarGeom& g, uint8_t* lds, uint64_t i0, uint64_t i1) {
+  const uint64_t nb = i1 - i0;
+  if (nb == 0 || nb > kPermMax) return nullptr;
+  constexpr uint32_t kT = kWave * NW;
+  uint32_t* bucket = reinterpret_cast<uint32_t*>(lds + kPermOff);
+  uint16_t* perm = reinterpret_cast<uint16_t*>(lds + kPermOff + 136u);
+  const uint32_t t = threadIdx.x;
+  if (t < 33) bucket[t] = 0u;
+  __syncthreads();
+  constexpr int kPer = (int)((kPermMax + kT - 1) / kT);
+  uint32_t key[kPer], rank[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint64_t x = (uint64_t)t + (uint64_t)q * kT;
+    key[q] = 0u;
+    rank[q] = 0u;
+    if (x < nb) {
+      const uint64_t L = g.lengths[i0 + x];
+      const uint32_t w = chunks_for(L) - (head_first(L) ? 1u : 0u);  // body chunks, 0..32
+      key[q] = 32u - min(w, 32u);
+      rank[q] = atomicAdd(&bucket[key[q]], 1u);
+    }
+  }
+  __syncthreads();
+  if (t < kWave) {  // exclusive prefix of the 33 buckets (key 0 = most chunks first)
+    const uint32_t v = t < 33 ? bucket[t] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+      if (t >= (uint32_t)o) x += y;
+    }
+    if (t < 33) bucket[t] = x - v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint64_t x = (uint64_t)t + (uint64_t)q * kT;
+    if (x < nb) perm[bucket[key[q]] + rank[q]] = (uint16_t)x;
+  }
+  __syncthreads();
+  return perm;
+}
+
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(VarGeom gv, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes > kPermLdsBytes ? kFusedLdsBytes : kPermLdsBytes];
   NVL_FSTAMP(0);
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1, B0, B1;
-  bool long_bufs;
-  tiled_plan<kGenWaves>(lds, gv, ka, C0, C1, long_bufs, B0, B1);
+  bool long_bufs, multi;
+  tiled_plan<kGenWaves>(lds, gv, ka, C0, C1, long_bufs, B0, B1, multi);
   // The range is uniform, but the 64-bit divisions that made it ran on the
   // VALU: pin it to SGPRs, or it stays in VGPRs through the main loop and
   // that spills (25 VGPRs, 108 B/lane scratch, cfg3 287 -> 430 us).
@@ -2325,7 +2390,10 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     // whole buffers: no records, so no edge fold either -- no grid-wide
     // hand-off (its sc1 stores, drain and counter round trip cost ~5 us of
     // tail; the stream's counter is left untouched, i.e. zero)
-    run_bufs<kGenWaves>(gv, ka, lds, uniform_u64(B0), uniform_u64(B1));
+    B0 = uniform_u64(B0);
+    B1 = uniform_u64(B1);
+    const uint16_t* perm = multi ? lpt_order<kGenWaves>(gv, lds, B0, B1) : nullptr;
+    run_bufs<kGenWaves>(gv, ka, lds, B0, B1, perm);
     return;
   }
   run_general<kGenWaves>(g, ka, lds);

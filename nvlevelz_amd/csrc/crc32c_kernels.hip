@@ -1187,12 +1187,15 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
 #endif
   const uint32_t GS = (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (NVL_BUFS_DIV * NW)));  // buffers per group
 #ifndef NVL_BUFS_TAIL
-#define NVL_BUFS_TAIL 64  // the range's last buffers go out one per group
+#define NVL_BUFS_TAIL 0  // single-buffer groups for the range's last buffers (tuning knob)
 #endif
-  // Groups of GS buffers, then single-buffer groups for the range's last
-  // kBT buffers, so a workgroup's waves finish within about one buffer of each
-  // other (with GS-buffer groups to the end they finished 12 us apart on
-  // 10^5 x 4097 B and 27 us apart on config 3: tools/diag/bstamps.py).
+  // Groups of GS buffers (optionally single-buffer groups for the range's
+  // last kBT buffers).  The singles once evened out the waves' ends (12 us
+  // apart on 10^5 x 4097 B, 27 us on config 3); with the buffers handed out
+  // most-chunks-first (lpt_order) and the next group's metadata prefetched
+  // they only cost single-chunk steps: 64 -> 0 took 10^5 x 4097 B from 101
+  // to 91 us per call and 10^5 x 3364..4109 B from 124 to 115 us, config 3
+  // unchanged within the box's spread (tools/diag/ab_variants.sh, same box).
   const uint64_t kBT = NVL_BUFS_TAIL;
   const uint64_t nbig = nb > kBT * 2 ? (nb - kBT) / GS : 0;  // GS-buffer groups
   const uint64_t ngroups = nbig + (nb - nbig * GS);

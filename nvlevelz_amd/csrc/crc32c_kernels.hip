@@ -2543,9 +2543,13 @@ static inline uint32_t chunks_of(uint64_t len) { return dev::chunks_for(len); }
 
 // The head kernel over a geometry's n buffers; its dispatch records
 // ev_start when given (it is then the call's first kernel).
+#ifndef NVL_HEAD_GRID_MULT
+#define NVL_HEAD_GRID_MULT 1  // head kernel workgroups per CU (tuning knob; the fused plan takes <= 1023 tiles)
+#endif
 static inline uint32_t head_grid(int num_cu, uint64_t n) {
   const uint64_t per_wg = 8u * dev::kWavesPerWG;  // at least ~8 buffers per wave
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_cu, (n + per_wg - 1) / per_wg));
+  const uint64_t cap = std::min<uint64_t>((uint64_t)num_cu * NVL_HEAD_GRID_MULT, dev::kMaxTiles);
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, (n + per_wg - 1) / per_wg));
 }
 
 template <class G>

@@ -207,6 +207,43 @@ def test_varlen_random_edges(dev, C, port):
     assert np.array_equal(got, np.array([port.mask(int(x)) for x in want[perm]], dtype=np.uint32))
 
 
+def test_varlen_long_heads_page_edges(dev, C, port):
+    """Long heads (1025..4095 B), which the head kernel runs as whole chunks
+    with row loads reaching up to 12 bytes below the buffer's 16-B granule,
+    at starts around 4 KiB page boundaries of the absolute address: a buffer
+    starting in a page's first granule takes the lane-group path instead
+    (tests/kernel_model.py long_head).  1..3 chunks, random inits."""
+    rng = np.random.default_rng(4096)
+    total = 260 * 4096
+    host = port.fill(0xF00D, 0, total)
+    buf = torch.from_numpy(host).to(dev)
+    base = buf.data_ptr()
+    page_offs = [0, 1, 3, 4, 15, 16, 17, 28, 31, 32, 4079, 4080, 4095]
+    offs, lens = [], []
+    for k in range(400):
+        po = page_offs[k % len(page_offs)]
+        hl = int(rng.choice([1025, 1026, 1100, 2048, 3000, 4000, 4080, 4081, 4094, 4095]))
+        J = int(rng.choice([1, 1, 2, 3]))
+        page = 1 + (k * 37) % 240
+        offs.append(page * 4096 + (po - base) % 4096)
+        lens.append(hl + 4096 * (J - 1))
+    offs = np.array(offs, dtype=np.int64)
+    lens = np.array(lens, dtype=np.int64)
+    assert int((offs + lens).max()) < total
+    inits = rng.integers(0, 2**32, size=len(offs), dtype=np.uint64).astype(np.uint32)
+    got = _varlen(C, dev, buf, offs, lens, init=inits)
+    want = port.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64), inits)
+    assert np.array_equal(got, want)
+    # the same heads as a fixed-stride batch (the head kernel with FixedGeom)
+    for hl in (1025, 3000, 4095):
+        for po in (0, 16, 4080):
+            off = 4096 + (po - base) % 4096
+            n = 50
+            got = _u32(C.extend_fixed(buf, hl + 7, hl, n, 0x5A5A5A5A, base_offset=off))
+            ref = port.fixed(host[off:], hl + 7, hl, n, np.full(n, 0x5A5A5A5A, dtype=np.uint32))
+            assert np.array_equal(got, ref), (hl, po)
+
+
 def test_varlen_many_tiny(dev, C, port):
     rng = np.random.default_rng(3)
     n = 200_000

@@ -1586,7 +1586,7 @@ constexpr uint32_t kLongOk = 1u << 16, kLongLast = 1u << 17;  // long-head tags:
 // pass earlier, before those chunk loads -- into positions, pulls the pair
 // after it and issues its metadata loads, issues the next pair's chunk loads,
 // then runs the chains.  Past the end of the list a slot is a dummy chunk in
-// the table blob (loaded, not written).
+// the table blob (loaded, not written; a pair of two dummies is not run).
 template <class G>
 __device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t* lds, const LaneBase& lb,
                                            uint64_t sub0, uint32_t* lcnt, const uint16_t* llist) {
@@ -1646,6 +1646,9 @@ __device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t*
   load_general(ceA, true, pA, lane, cA);
   load_general(ceB, true, pB, lane, cB);
   while (true) {
+    // a pair wholly past the list's end is not run (its loads, of the table
+    // blob, just drain)
+    if (!(tA & kLongOk)) break;
     uint32_t w[2][16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[0][q] = cA.d[q];

@@ -271,6 +271,24 @@ def test_varlen_plan_paths(dev, C, port, n):
     assert np.array_equal(got, want)
 
 
+def test_varlen_lpt_fallback(dev, C, port):
+    """Scheduler C hands a workgroup's buffers out most-chunks-first when the
+    range holds multi-chunk buffers and at most kPermMax (1792) buffers;
+    700k mostly tiny buffers with 2 % of 9000 B ones put ~2700 buffers in
+    every workgroup's range: the natural-order fallback."""
+    rng = np.random.default_rng(1792)
+    n = 700_000
+    lens = np.where(rng.random(n) < 0.98, rng.integers(0, 65, n), 9000).astype(np.int64)
+    offs = (np.cumsum(lens + 3) - lens).astype(np.int64)
+    total = int(offs[-1] + lens[-1]) + 64
+    host = port.fill(0x1792, 0, total)
+    buf = torch.from_numpy(host).to(dev)
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    got = _varlen(C, dev, buf, offs, lens, init=inits)
+    want = port.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64), inits)
+    assert np.array_equal(got, want)
+
+
 def test_empty_batches(dev, C):
     buf = torch.zeros(16, dtype=torch.uint8, device=dev)
     assert C.extend_fixed(buf, 0, 0, 0).numel() == 0

@@ -25,11 +25,12 @@ exchange bytes; only the timing max and a verification digest cross ranks
 
 The JSON line adds
   roofline     -- dominant kernel: algorithmic bytes per launch (4096+4 B per
-                  block) / its mean duration from HIP events recorded on the
-                  launch stream, against the 8 TB/s HBM3E peak.  `traffic` is
-                  the PMC-measured HBM bytes per launch from
-                  profiles/pmc_traffic.json when present (rocprofv3, corrected
-                  per MI355X_MICROARCH.md §HBM), else null.
+                  block) / its average launch duration in the timed region
+                  (HIP events on the launch stream around the K launches / K),
+                  against the 8 TB/s HBM3E peak.  `traffic` is the committed
+                  PMC-measured HBM bytes per launch (profiles/pmc_traffic.json,
+                  rocprofv3 --pmc passes, corrected per MI355X_MICROARCH.md
+                  §HBM), labelled as such, else null.
   cpu_baseline -- the reference's own util/crc32c.cc + port/port_posix_sse.cc
                   (oracle/_ref, kind "reference"; the clean-room port, kind
                   "port", if _ref is absent) timed on this host's cores on a
@@ -136,37 +137,6 @@ def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int) -> dict
         "host_cpu": model, "host_nproc": os.cpu_count(), "physical_cores": phys, "affinity_cpus": logical,
         "_check": r_all,
     }
-
-
-def spawn_ranks(n: int) -> int:
-    """Start N ranks of this script (one per GPU) and wait for them.  Nothing
-    here touches a GPU; a rank that fails makes the others stop (by their
-    PIDs), and the first non-zero exit status is returned."""
-    import signal
-    import socket
-    import subprocess
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
-            live.remove(p)
-            if c != 0 and rc == 0:
-                rc = c
-                for q in live:
-                    q.send_signal(signal.SIGTERM)
-        time.sleep(0.05)
-    return rc
 
 
 def _varint(v: int) -> bytes:
@@ -301,35 +271,19 @@ def shim_bench(nblocks: int = 100_000) -> dict:
     return res
 
 
-def gather_global(res: np.ndarray, rank: int, N: int, total: int, dist, red_dev) -> np.ndarray:
-    """All ranks' CRCs (rank r holds global blocks r, r+N, ...) in global
-    block order, on every rank: ONE all_gather (RCCL on the box) of the
-    padded 4-byte results, outside the timed region."""
-    import torch
-    per = (total + N - 1) // N
-    mine = torch.zeros(per, dtype=torch.int32, device=red_dev)
-    mine[:res.size] = torch.from_numpy(res.view(np.int32)).to(red_dev)
-    parts = [torch.empty(per, dtype=torch.int32, device=red_dev) for _ in range(N)]
-    dist.all_gather(parts, mine)
-    allc = np.empty(total, dtype=np.uint32)
-    for r in range(N):
-        k = (total - r + N - 1) // N
-        allc[r::N] = parts[r][:k].cpu().numpy().view(np.uint32)
-    return allc
-
-
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))  # before anything touches a GPU
+    from nvlevelz_amd import launch  # (loads nothing: safe before the ranks exist)
+    rc = launch.main_or_spawn(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:  # launcher-less N > 1: this process only waited for its N ranks
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
 
-    from nvlevelz_amd import crc32c
+    from nvlevelz_amd import crc32c, shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    re_ = launch.rank_env()
+    world, rank, local = re_["world"], re_["rank"], re_["local_rank"]
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: running {world} rank(s)", file=sys.stderr)
         args.gpus = world
@@ -370,11 +324,12 @@ def main():
     out = batch.out
     step = batch.launch  # one C call per step; the host stays ahead of the GPU
 
-    for _ in range(args.warmup):
-        step()
+    step()
     torch.cuda.synchronize()
 
-    # --- verification (untimed) --------------------------------------------
+    # --- verification (untimed, before the warmup: the timed region starts
+    # right after the warmup launches, not after seconds of host-side checks
+    # with the GPU idle) -----------------------------------------------------
     verify = {}
     res = crc32c.to_u32(out)
     with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
@@ -384,7 +339,9 @@ def main():
         # little-endian CRC array, golden from the oracle pinned
         # to the reference (tests/golden/configs.json)
         g = golden[args.config]
-        allc = gather_global(res, rank, N, total, dist, red_dev) if N > 1 else res
+        # (shard.gather_crcs: ONE all_gather of the padded 4-byte results;
+        # tests/test_dist.py runs the same call over gloo)
+        allc = shard.gather_crcs(out[:n_local].to(red_dev), total) if N > 1 else res
         if rank == 0:
             d = crc32c.value(np.ascontiguousarray(allc, dtype="<u4").tobytes())
             verify.update({"crc0": hex(int(allc[0])), "crc0_ok": int(allc[0]) == g["crc_first"][0],
@@ -393,6 +350,10 @@ def main():
     elif rank == 0:
         verify["crc0"] = hex(int(res[0]))
         verify["crc0_ok"] = int(res[0]) == golden["cfg2"]["crc_first"][0]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
 
     # --- timed region ------------------------------------------------------
     # K back-to-back launches, nothing else enqueued between them.  Two HIP
@@ -413,12 +374,16 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
-    # Kernel-only durations, right after the timed region, same stream and
-    # buffers: K more back-to-back launches through nvl_crc32c_fixed_dev_timed,
-    # whose kernel dispatch records its own start/stop HIP events
-    # (hipExtLaunchKernel) -- what rocprofv3's kernel trace measures.  Kept
-    # out of the timed region: a dispatch that records events costs the queue
-    # a few us per launch (measured r02: 67.3 us kernels at 73.0 us per launch).
+    # Beside the in-regime figure, two untimed diagnostic passes (K launches
+    # each, after the timed region; tools/rocprof_summary.py splits them off a
+    # rocprofv3 trace of this command by launch order):
+    #  * dispatch events: nvl_crc32c_fixed_dev_timed, whose kernel dispatch
+    #    records its own start/stop events (hipExtLaunchKernel).  Back to back
+    #    these overlap: a dispatch's start stamp is taken while the previous
+    #    kernel still drains, so their mean can exceed the launch period and
+    #    is never used for the roofline;
+    #  * isolated launches: an ordinary event before and after each launch, so
+    #    every launch starts from an idle queue -- what one shim call sees.
     kev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
     for e in kev:
         e.record(stream)  # materialise the HIP events
@@ -426,15 +391,13 @@ def main():
         batch.launch_timed(kev[2 * k], kev[2 * k + 1])
     torch.cuda.synchronize()
     kern_ms = np.array([kev[2 * k].elapsed_time(kev[2 * k + 1]) for k in range(K)])
-    # Untimed: isolated launches (ordinary events around each: a marker
-    # packet before and after, so every launch starts from an idle queue).
-    iso = [torch.cuda.Event(enable_timing=True) for _ in range(2 * min(K, 50))]
-    for k in range(len(iso) // 2):
+    iso = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
+    for k in range(K):
         iso[2 * k].record(stream)
         step()
         iso[2 * k + 1].record(stream)
     torch.cuda.synchronize()
-    iso_ms = [iso[2 * k].elapsed_time(iso[2 * k + 1]) for k in range(len(iso) // 2)]
+    iso_ms = [iso[2 * k].elapsed_time(iso[2 * k + 1]) for k in range(K)]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -446,10 +409,19 @@ def main():
         total_blocks = n_local
 
     value = total_blocks * BLOCK * K / elapsed / 2**30
-    mean_kern_s = float(kern_ms.mean()) / 1e3
+    # Roofline: the kernel's average launch duration in the timed region
+    # itself = the HIP-event interval on the launch stream / K.  Launches are
+    # serialised on one stream with nothing between them, so this period
+    # bounds the kernel's own duration from above (frac is a lower bound on
+    # the kernel's fraction) and can never exceed the wall-clock step.
+    period_s = region_ms / 1e3 / K
+    step_s = elapsed / K
+    assert period_s <= step_s * 1.0001, (period_s, step_s)  # events inside the wall-clock bracket
     alg_bytes = n_local * (BLOCK + 4)  # every input byte once + 4 B CRC out
-    achieved = alg_bytes / mean_kern_s / 1e9
-    traffic = None
+    achieved = alg_bytes / period_s / 1e9
+    frac = achieved / HBM_PEAK_GBS
+    frac_wall = alg_bytes / step_s / 1e9 / HBM_PEAK_GBS  # the same over the driver-visible wall clock
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
@@ -457,6 +429,7 @@ def main():
                 pj = json.load(f)
             if pj.get("blocks") == n_local:
                 traffic = pj.get("hbm_bytes_per_launch")
+                traffic_src = pj.get("source")
         except (OSError, ValueError):
             traffic = None
 
@@ -502,19 +475,27 @@ def main():
             "config": {"workload": workload, "blocks_per_gpu": n_local, "block_bytes": BLOCK,
                        "parallelism": f"{N} independent shard(s), no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(frac, 4), "traffic": traffic,
+                         "traffic_source": (f"committed PMC, not measured in this run: profiles/pmc_traffic.json "
+                                            f"({traffic_src}; rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                                            f"this kernel and batch, gfx950 corrections per MI355X_MICROARCH.md)"
+                                            if traffic is not None else None),
                          "kernel": kern, "alg_bytes_per_launch": alg_bytes,
-                         "mean_kernel_us": round(mean_kern_s * 1e6, 2),
-                         "median_kernel_us": round(float(np.median(kern_ms)) * 1e3, 2),
-                         "kernel_what": "kernel-only duration of each of K back-to-back launches run right after the "
-                                        "timed region (same stream, buffers and batch), from HIP events recorded by "
-                                        "the kernel dispatch itself (hipExtLaunchKernel); achieved = alg_bytes / mean",
-                         "mean_launch_us": round(region_ms / K * 1e3, 2),
-                         "mean_launch_what": "HIP events bracketing the K timed launches / K (incl. inter-launch gaps)",
+                         "mean_kernel_us": round(period_s * 1e6, 2),
+                         "kernel_what": "average launch duration over the K timed launches: HIP events recorded on "
+                                        "the launch stream around the timed region / K (back-to-back launches, "
+                                        "nothing else enqueued; an upper bound on the kernel's own time); "
+                                        "achieved = alg_bytes / this",
+                         "frac_wall": round(frac_wall, 4),
+                         "frac_wall_what": "alg_bytes / ms_per_step (wall clock incl. synchronize) / peak",
+                         "dispatch_event_mean_us": round(float(kern_ms.mean()) * 1e3, 2),
+                         "dispatch_event_what": "untimed diagnostic: start/stop events recorded by each kernel "
+                                                "dispatch (hipExtLaunchKernel), K back-to-back launches; they overlap "
+                                                "the previous kernel's drain, so not used for frac",
                          "isolated_median_us": round(float(np.median(iso_ms)) * 1e3, 2),
                          "isolated_frac": round(alg_bytes / (float(np.median(iso_ms)) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "isolated_what": "untimed pass: ordinary events before and after each launch (the launch "
-                                          "starts from an idle queue, as a single shim call does); median"},
+                         "isolated_what": "untimed diagnostic: ordinary events before and after each launch (the "
+                                          "launch starts from an idle queue, as a single shim call does); median"},
             "cpu_baseline": cpu,
             "verify": verify,
         }

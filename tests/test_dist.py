@@ -1,9 +1,17 @@
 """Round-robin sharding + result gather over torch.distributed, world_size 2
-on the CPU (gloo).  On the GPU box the same code runs over RCCL; per-rank
-checksums there come from the HIP kernels -- here the checker computes them,
-so this exercises the partition, the single all_gather and the reassembly."""
+and 3 on the CPU (gloo).  On the GPU box the same code runs over RCCL with
+per-rank checksums from the HIP kernels; here every rank checksums its shard
+with the engine's host path (libnvl_crc32c.so nvl_crc32c_value) and the
+oracle only checks the reassembled result.
+
+test_spawned_ranks_*: the launcher-less path of ``bench.py --gpus N``
+(nvlevelz_amd.launch.spawn_ranks, no torchrun) with tests/dist_rank_worker.py
+as the rank body: 2 ranks reassemble BASELINE config 2's golden digest."""
 import os
 import socket
+import subprocess
+import sys
+import time
 
 import numpy as np
 import pytest
@@ -24,7 +32,7 @@ def _free_port():
 def _worker(rank, world, port, n, result_q):
     import torch.distributed as dist
     import oracle
-    from nvlevelz_amd import shard
+    from nvlevelz_amd import crc32c, shard
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -36,7 +44,8 @@ def _worker(rank, world, port, n, result_q):
         # this rank's resident shard: block k = global block ids[k] of the stream
         buf = np.concatenate([p.fill(0x5EED0001, int(i) * L, L) for i in ids]) if ids.size else \
             np.zeros(0, dtype=np.uint8)
-        local = p.fixed(buf, L, L, ids.size) if ids.size else np.zeros(0, dtype=np.uint32)
+        # the engine's host path (the reference's Value() replacement), block by block
+        local = np.array([crc32c.value(buf[k * L:(k + 1) * L]) for k in range(ids.size)], dtype=np.uint32)
         t = torch.from_numpy(local.view(np.int32).copy())
         full = shard.gather_crcs(t, n)
         result_q.put((rank, full.tolist(), shard.digest(full)))
@@ -79,3 +88,56 @@ def test_partition_math():
             assert sorted(ids) == list(range(n))
     parts = [np.arange(0, 10, 3), np.arange(1, 10, 3), np.arange(2, 10, 3)]
     assert shard.interleave(parts, 10).tolist() == list(range(10))
+
+
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_rank_worker.py")
+
+
+def _spawn(n_ranks, args, timeout=300):
+    """Run the rank worker through launch.spawn_ranks in a fresh interpreter
+    (as bench.py's parent would: no torchrun, no WORLD_SIZE)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    code = ("import sys; sys.path.insert(0, %r); from nvlevelz_amd import launch; "
+            "sys.exit(launch.spawn_ranks(%d, [sys.executable, '-u', %r] + %r, grace_s=5.0))"
+            % (os.path.dirname(os.path.dirname(WORKER)), n_ranks, WORKER, [str(a) for a in args]))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout)
+    return r, time.monotonic() - t0
+
+
+def test_spawned_ranks_reassemble_cfg2_digest():
+    g = load_golden("configs")["cfg2"]
+    r, _ = _spawn(2, [100_000, hex(g["digest"])])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("digest %#010x" % g["digest"]) == 2, r.stdout
+
+
+def test_spawned_ranks_small_world3():
+    import oracle
+    p = oracle.port()
+    n = 1001
+    whole = p.fixed(p.fill(0x5EED0001, 0, n * 4096), 4096, 4096, n)
+    r, _ = _spawn(3, [n, hex(p.digest(whole))])
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_spawned_rank_failure_stops_the_others():
+    # rank 1 exits 7 before the rendezvous; rank 0 would wait in
+    # init_process_group for 30 minutes unless the spawner stops it
+    r, el = _spawn(2, [16, "0x0", 1], timeout=120)
+    assert r.returncode == 7, r.stdout + r.stderr
+    assert el < 60
+
+
+def test_launch_module_loads_no_hip():
+    """The spawner's parent must not touch a GPU: importing the launch module
+    (and the package) loads neither libnvl_crc32c.so nor torch."""
+    code = ("import sys; sys.path.insert(0, %r); import nvlevelz_amd.launch as l; "
+            "print(int(l.rank_env()['world'])); "
+            "print(any('nvl_crc32c' in m or m == 'torch' for m in sys.modules)); "
+            "import os; print(any('libnvl_crc32c' in x for x in open('/proc/self/maps').read().split()))"
+            % os.path.dirname(os.path.dirname(WORKER)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["1", "False", "False"], r.stdout

@@ -1,12 +1,19 @@
 #!/bin/bash
-# One GPU call of round-2 work: parity tests, the default bench line, the
-# self-spawned 2-rank cfg5 rehearsal (gloo, ranks sharing one GPU), and a
-# rocprofv3 kernel trace of the whole-table verify shim bench.
-#   bash tools/gpu_round.sh TAG [steps...]    steps: tests bench spawn shims (default: all)
+# One GPU call of round work, every step under its own time limit, stopping
+# at the first failure.
+#   bash tools/gpu_round.sh TAG [steps...]
+# steps:
+#   tests   pytest -m gpu (parity)
+#   bench   the driver's exact command: python3 bench.py --gpus 1 --steps 20 --warmup 5
+#   prof    rocprofv3 --kernel-trace --stats of that same command (summary split by phase)
+#   spawn   self-spawned 2-rank rehearsals without torchrun (gloo, ranks sharing one GPU):
+#           cfg5 (full 10^7-block digest through shard.gather_crcs) and cfg2
+#   configs tools/bench_configs.py over 2,3,4,v,g,r
+#   shims   rocprofv3 kernel trace of the whole-table verify shim bench
 set -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 shift
-STEPS=${*:-tests bench spawn shims}
+STEPS=${*:-tests bench prof spawn configs}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
@@ -23,19 +30,24 @@ run() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
-    bench) run bench 400 python bench.py ;;
-    spawn) NVL_BENCH_BACKEND=gloo run spawn 400 python bench.py --gpus 2 --config cfg5 --steps 20 --warmup 3 ;;
-    cfg5) run cfg5 400 python bench.py --config cfg5 --steps 50 --warmup 5 --no-cpu --no-e2e ;;
+    tests) run pytest 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
+    bench) run bench 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench100) run bench100 300 python3 bench.py --gpus 1 --steps 300 --warmup 100 --no-cpu --no-e2e ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp
+      run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
+        python3 $R/bench.py --gpus 1 --steps 20 --warmup 5
+      cd $R
+      tr=$(ls $OUT/prof_$TAG/*/run_kernel_trace.csv $OUT/prof_$TAG/run_kernel_trace.csv 2>/dev/null | head -1)
+      python3 tools/rocprof_summary.py "$tr" $OUT/prof_summary_$TAG.json 20 5 $OUT/prof_timed_stats_$TAG.csv ;;
+    spawn)
+      NVL_BENCH_BACKEND=gloo run spawn_cfg5 400 python3 bench.py --gpus 2 --config cfg5 --steps 10 --warmup 2 --no-cpu --no-e2e
+      NVL_BENCH_BACKEND=gloo run spawn_cfg2 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-e2e ;;
+    configs) run configs 600 python3 tools/bench_configs.py --configs 2,3,4,v,g,r ;;
     shims)
       cd /tmp && export TMPDIR=/tmp
       run shims 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_shims_$TAG -o run -- \
         python3 $R/bench.py --shims --no-cpu --no-e2e --steps 20 --warmup 5
-      cd $R ;;
-    prof)
-      cd /tmp && export TMPDIR=/tmp
-      run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-        python3 $R/bench.py --no-cpu --no-e2e --steps 100 --warmup 20
       cd $R ;;
   esac
 done

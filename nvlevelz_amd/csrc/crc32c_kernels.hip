@@ -74,11 +74,26 @@ constexpr uint32_t kGSlice = 0, kGComb = 1024, kGX2n = 1024 + 6144 + 1024;  // c
 // Wave-uniform copies (lane 0's value in SGPRs).  readfirstlane returns int:
 // each half goes through uint32_t so that a low half >= 2^31 is not
 // sign-extended into the high half (a device address usually has bit 31 set).
-__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+// These four helpers are the ONLY places the kernels may call
+// __builtin_amdgcn_readfirstlane / __builtin_amdgcn_readlane
+// (tests/test_kernel_source.py enforces it): the 32-bit forms refuse wider
+// operands at compile time, the 64-bit forms move two uint32_t halves.
+template <class T>
+__device__ __forceinline__ uint32_t uniform_u32(T v) {
+  static_assert(sizeof(T) <= 4, "uniform_u32 of a 64-bit value: use uniform_u64");
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 }
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
   return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | (uint64_t)uniform_u32((uint32_t)v);
+}
+// lane j's value (j wave-uniform)
+template <class T>
+__device__ __forceinline__ uint32_t lane_u32(T v, uint32_t j) {
+  static_assert(sizeof(T) <= 4, "lane_u32 of a 64-bit value: use lane_u64");
+  return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)j);
+}
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t j) {
+  return ((uint64_t)lane_u32((uint32_t)(v >> 32), j) << 32) | (uint64_t)lane_u32((uint32_t)v, j);
 }
 
 // cross-lane helpers (all called with EXEC = all 64 lanes)
@@ -113,24 +128,12 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-#if defined(NVL_ABL_STRIDED) || defined(NVL_ABL_NOLOAD)
-#define NVL_ABL_LAYOUT_STRIDED 1
-#else
-#define NVL_ABL_LAYOUT_STRIDED 0
-#endif
-
 typedef const u32x4 __attribute__((address_space(1))) * gvec_ptr;
 
 // 16-byte streaming load from global memory (read-once data: non-temporal
 // hint).  The explicit address space keeps it a global_load (a flat_load would
 // also count in lgkmcnt and serialise against the LDS lookups).
-__device__ __forceinline__ u32x4 ld16(uintptr_t addr) {
-#if defined(NVL_ABL_NO_NT)
-  return *(gvec_ptr)addr;
-#else
-  return __builtin_nontemporal_load((gvec_ptr)addr);
-#endif
-}
+__device__ __forceinline__ u32x4 ld16(uintptr_t addr) { return __builtin_nontemporal_load((gvec_ptr)addr); }
 
 // The same through the caches: the head kernel's lane-group loads touch each
 // line from several instructions (lanes 64 bytes apart), so non-temporal
@@ -180,11 +183,7 @@ __device__ __forceinline__ uint32_t slice4_x(const uint8_t* lds, uint32_t x, uin
 
 // slice4(x) ^ next -- the chain step with the following word folded in.
 __device__ __forceinline__ uint32_t slice4_next(const uint8_t* lds, uint32_t x, uint32_t next, const LaneBase& lb) {
-#if defined(NVL_NO_XOR3)
-  return slice4(lds, x, lb) ^ next;
-#else
   return slice4_x(lds, x, next, lb);  // two v_bitop3 instead of four v_xor (tools/ab_bench.py: -2 us on cfg2)
-#endif
 }
 
 
@@ -525,21 +524,6 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
   const uintptr_t ce = chunk_end(bi, c);
   const uint32_t lo = lane_load_off(lane);
   if constexpr (M == kAligned) {
-#if defined(NVL_ABL_NOLOAD)  // ablation: synthetic data, no global loads
-#pragma unroll
-    for (int k = 0; k < 16; ++k) ch.d[k] = (uint32_t)(ce >> 4) * 2654435761u + (uint32_t)(k * 40503 + lane);
-    return;
-#endif
-#if defined(NVL_LD_AUX)  // tuning build: buffer loads with explicit cache-policy bits
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(ce - kChunk), (short)0, (int)kChunk, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(1024u * (uint32_t)j + lo), 0, NVL_LD_AUX);
-      ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
-    }
-    return;
-#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const u32x4 v = ld16(ce - kChunk + 1024u * (uint32_t)j + lo);
@@ -636,7 +620,6 @@ __device__ __forceinline__ void head_fix(uint32_t (&w)[16], uint32_t rel, uint32
 __device__ __forceinline__ void realign_general(uintptr_t ce, bool hd, uintptr_t p, uint32_t s, int lane,
                                                 const Chunk& ch, uint32_t (&w)[16]) {
   const uintptr_t cs = ce - kChunk;
-#if !defined(NVL_ABL_NOREALIGN)
   // (Unconditional -- alignbyte by 0 keeps the low word -- spares the
   // compiler's register copies at the join but measured slower: scheduler C
   // 10^5 x 4097 B 85.5 -> 91.5 us, config 3 223 -> 235 us, same box.)
@@ -647,13 +630,10 @@ __device__ __forceinline__ void realign_general(uintptr_t ce, bool hd, uintptr_t
     for (int k = 0; k < 15; ++k) w[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
     w[15] = __builtin_amdgcn_alignbyte(nx, w[15], r);
   }
-#endif
   if (!hd) {
     if (cs < p + 4 && lane == 0) w[0] ^= s >> (8u * (uint32_t)(cs - p));
   } else {
-#if !defined(NVL_ABL_HEADFIX)
     head_fix(w, (uint32_t)(p - cs), s, lane);
-#endif
   }
 }
 
@@ -664,9 +644,7 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
                                             uint32_t (&w)[16], uint32_t (&ov)[4]) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
-#if !defined(NVL_ABL_NOLOAD)
   row_transpose(w);
-#endif
   if constexpr (M == kAligned) {
     if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0, word 0
   } else {
@@ -685,28 +663,6 @@ template <int U, bool OPQ>
 __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16], int lane,
                                        uint32_t (&raw)[U]) {
   uint32_t crc[U];
-#if defined(NVL_ABL_NOCOMPUTE)  // ablation: keep the loads live, skip every lookup
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    crc[u] = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) crc[u] ^= w[u][k];
-    raw[u] = crc[u] ^ lane_xor<5>(crc[u]);
-  }
-  return;
-#endif
-#if defined(NVL_ABL_HALF)  // ablation: two independent 8-step half chains per lane (wrong combine)
-  if constexpr (U == 1) {
-    uint32_t a = w[0][0], b = w[0][8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      a = slice4_next(lds, a, k < 7 ? w[0][k + 1] : 0u, lb);
-      b = slice4_next(lds, b, k < 7 ? w[0][k + 9] : 0u, lb);
-    }
-    crc[0] = a ^ b;
-  } else
-#endif
-  {
 #pragma unroll
   for (int u = 0; u < U; ++u) crc[u] = w[u][0];
 #pragma unroll
@@ -714,12 +670,6 @@ __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, c
 #pragma unroll
     for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
   }
-  }
-#if defined(NVL_ABL_NOFOLD)  // ablation: chains only, no butterfly
-#pragma unroll
-  for (int u = 0; u < U; ++u) raw[u] = crc[u] ^ dpp_xor1(crc[u]);
-  return;
-#endif
   // Lane = stream position P: lane bit k steps 64*2^k bytes (comb table k).
   // Bits 0 and 1 go first: afterwards the lanes of a quad hold equal values,
   // which fold_level's quad-spread byte lookups rely on.
@@ -844,29 +794,13 @@ __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane) {
   if (lane == 0)
     v = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + kCtrOff), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
-  return __builtin_amdgcn_readfirstlane(v);
+  return uniform_u32(v);
 }
 
-#if defined(NVL_DIAG_STAMPS)
-// Diagnostic build only: per-wave {start, after-fill, end} s_memrealtime
-// stamps and {XCC id, units}, read back with nvl_diag_stamps().
-__device__ unsigned long long g_stamps[4 * 65536];
-#define NVL_STAMP0() const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime(); uint32_t nproc = 0
-#define NVL_STAMP1() const unsigned long long ts1 = __builtin_amdgcn_s_memrealtime()
-#define NVL_COUNT() (++nproc)
-#define NVL_STAMP_END()                                                                     \
-  do {                                                                                      \
-    const uint32_t wave_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);              \
-    if ((threadIdx.x & 63) == 0 && wave_ < 65536) {                                         \
-      unsigned xcc_;                                                                        \
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
-      g_stamps[4 * wave_ + 0] = ts0;                                                        \
-      g_stamps[4 * wave_ + 1] = ts1;                                                        \
-      g_stamps[4 * wave_ + 2] = __builtin_amdgcn_s_memrealtime();                           \
-      g_stamps[4 * wave_ + 3] = ((unsigned long long)xcc_ << 32) | nproc;                   \
-    }                                                                                       \
-  } while (0)
-#else
+// Per-wave timeline hooks (NVL_STAMP0 / NVL_STAMP1 / NVL_COUNT /
+// NVL_STAMP_END): no-ops here; tools/diag/stamps.h defines them for a
+// diagnostic variant build (make variant VFLAGS="-include .../stamps.h").
+#ifndef NVL_STAMP0
 #define NVL_STAMP0() do {} while (0)
 #define NVL_STAMP1() do {} while (0)
 #define NVL_COUNT() do {} while (0)
@@ -889,7 +823,7 @@ template <int U, int NW = kWavesPerWG, int M = kAligned>
 __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
   const uint64_t B0 = g.n * blockIdx.x / gridDim.x;
   const uint64_t B1 = g.n * (blockIdx.x + 1) / gridDim.x;
   // The range's last kTail buffers are single-buffer units: a CU's waves
@@ -988,7 +922,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   constexpr int kStep = M == kAligned ? NVL_UNIT_STEP_ALIGNED : NVL_UNIT_STEP;
   static_assert(M == kAligned || kStep == 1, "the kGeneral loop skips head chunks one step at a time");
   const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
   const uint64_t T = g.total();
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG, ub1 = ub0 + kUnitsPerWG;
   constexpr bool kFastDiv = M != kAligned;
@@ -1180,7 +1114,7 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
                                          const uint16_t* perm = nullptr) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
   const uint64_t nb = i1 > i0 ? i1 - i0 : 0;
 #ifndef NVL_BUFS_DIV
 #define NVL_BUFS_DIV 4  // about this many GS-buffer groups per wave
@@ -1270,12 +1204,10 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
       }
       const uint32_t j = (uint32_t)__builtin_ctzll(todo);
       todo &= todo - 1u;
-      cp = ((uintptr_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lp >> 32), (int)j) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lp, (int)j);
-      cL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lL >> 32), (int)j) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lL, (int)j);
-      cx = (uint32_t)__builtin_amdgcn_readlane((int)ls, (int)j);
-      ci = i0 + (uint32_t)__builtin_amdgcn_readlane((int)lr, (int)j);
+      cp = (uintptr_t)lane_u64((uint64_t)lp, j);
+      cL = lane_u64(lL, j);
+      cx = lane_u32(ls, j);
+      ci = i0 + lane_u32(lr, j);
       cJ = chunks_for(cL);
       cfb = head_first(cL) ? 1u : 0u;
       cc = cfb;
@@ -1591,14 +1523,14 @@ template <class G>
 __device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t* lds, const LaneBase& lb,
                                            uint64_t sub0, uint32_t* lcnt, const uint16_t* llist) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nl = (uint32_t)__builtin_amdgcn_readfirstlane((int)lcnt[0]);
+  const uint32_t nl = uniform_u32(lcnt[0]);
   if (nl == 0) return;
   const uintptr_t safe = (uintptr_t)ka.tables;
   const uint32_t* const ibase = g.init ? g.init : reinterpret_cast<const uint32_t*>(safe);
   auto pull = [&]() -> uint32_t {
     uint32_t v = 0;
     if (lane == 0) v = atomicAdd(&lcnt[1], 2u);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    return uniform_u32(v);
   };
   // metadata of list entries k, k+1 (raw loads; all lanes the same address)
   uint32_t k = pull();
@@ -1619,7 +1551,7 @@ __device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t*
   // a position from loaded metadata (uniform: lane 0's copy)
 #define NVL_POS(MO, ML, MI, MJ, CE, P, S, TAG)                                                          \
   do {                                                                                                 \
-    TAG = (uint32_t)__builtin_amdgcn_readfirstlane((int)(MJ));                                          \
+    TAG = uniform_u32((uint32_t)(MJ));                                                                 \
     const uint64_t L_ = uniform_u64(ML);                                                               \
     const uint32_t J_ = chunks_for(L_);                                                                \
     P = (TAG & kLongOk) ? g.base_addr() + uniform_u64(MO) : safe + 16u;                                 \
@@ -1666,12 +1598,7 @@ __device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t*
     load_general(ceA, true, pA, lane, cA);
     load_general(ceB, true, pB, lane, cB);
     uint32_t raws[2];
-#if defined(NVL_ABL_LONGNOCHAIN)
-    raws[0] = w[0][0] ^ w[0][15];
-    raws[1] = w[1][0] ^ w[1][15];
-#else
     chains<2, false>(lds, lb, w, lane, raws);
-#endif
     NVL_WRITE(uA, raws[0]);
     NVL_WRITE(uB, raws[1]);
     if (!(uB & kLongOk)) break;  // (entries are drained in order per wave: uA empty implies uB empty)
@@ -1681,20 +1608,10 @@ __device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t*
 #undef NVL_META
 }
 
-#if defined(NVL_DIAG_HSTAMPS)
-// Diagnostic build only: per-wave {start, tables ready, end, long-head cycles}
-// of the head kernel (s_memrealtime), read back with nvl_diag_hstamps().
-__device__ unsigned long long g_hstamps[4 * 65536];
-#endif
-
 template <class G>
 __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* lds) {
-#if defined(NVL_DIAG_HSTAMPS)
-  const unsigned long long hs0 = __builtin_amdgcn_s_memrealtime();
-  unsigned long long hs_long = 0;
-#endif
   const int lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
   // the workgroup's buffers: its plan tile when there is one
   uint64_t w0 = g.n * blockIdx.x / gridDim.x, w1 = g.n * (blockIdx.x + 1) / gridDim.x;
   bool tables = true;
@@ -1732,9 +1649,6 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     fill_lds<kWavesPerWG>(lds, ka.tables);
     __syncthreads();
   }
-#if defined(NVL_DIAG_HSTAMPS)
-  const unsigned long long hs1 = __builtin_amdgcn_s_memrealtime();
-#endif
   for (uint64_t sub0 = w0; sub0 < w1; sub0 += kHeadSub) {  // (workgroup-uniform trip count)
     const uint64_t sub1 = min(w1, sub0 + kHeadSub);
     uint64_t gb, ge;
@@ -1771,7 +1685,7 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       if (mco) {  // append to the workgroup's list (index within the sub-range)
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(&lcnt[0], (uint32_t)__builtin_popcountll(mco));
-        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        base = uniform_u32(base);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mco >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mco, 0u));
         if (coal) llist[base + rank] = (uint16_t)(i - sub0);
       }
@@ -1861,29 +1775,12 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     }
     if (tables) {  // (workgroup-uniform)
       __syncthreads();  // the list is complete
-#if defined(NVL_DIAG_HSTAMPS)
-      const unsigned long long hl0 = __builtin_amdgcn_s_memrealtime();
-#endif
       long_heads(g, ka, lds, lb, sub0, lcnt, llist);
-#if defined(NVL_DIAG_HSTAMPS)
-      hs_long += __builtin_amdgcn_s_memrealtime() - hl0;
-#endif
       __syncthreads();  // drained
       if (threadIdx.x < 2) lcnt[threadIdx.x] = 0u;
       __syncthreads();
     }
   }
-#if defined(NVL_DIAG_HSTAMPS)
-  {
-    const uint32_t wave_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (lane == 0 && wave_ < 65536) {
-      g_hstamps[4 * wave_ + 0] = hs0;
-      g_hstamps[4 * wave_ + 1] = hs1;
-      g_hstamps[4 * wave_ + 2] = __builtin_amdgcn_s_memrealtime();
-      g_hstamps[4 * wave_ + 3] = hs_long;
-    }
-  }
-#endif
 }
 
 template <class G>
@@ -1907,10 +1804,6 @@ template <int M>
 __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
   if constexpr (M == kAligned) {
-#if defined(NVL_DIAG_ONLY_PAIRS)  // ISA inspection of scheduler A alone
-    run_pairs<NVL_FAST_U>(g, ka, lds);
-    return;
-#endif
     if (g.J == 1) {
       run_pairs<NVL_FAST_U>(g, ka, lds);
       return;
@@ -2090,7 +1983,7 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_small(const uint64_t
 // costs tens of steps, not thousands of serial ones.
 __global__ __launch_bounds__(256) void crc32c_fixup_kernel(const Rec* __restrict__ recs, uint32_t nw,
                                                            uint32_t* __restrict__ out, uint32_t flags) {
-  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t w = uniform_u32(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   if (w >= nw) return;
   const Rec h = recs[2 * (uint64_t)w];
@@ -2182,13 +2075,6 @@ struct VarGeomFused {
 };
 
 
-#if defined(NVL_DIAG_FUSED)
-__device__ unsigned long long g_fstamps[8 * 1024];
-#define NVL_FSTAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < 1024) g_fstamps[8 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime()
-#else
-#define NVL_FSTAMP(k) do {} while (0)
-#endif
 
 // Plan, part 2, from the head kernel's tiles (tile_scan), in the LDS the
 // tables later occupy: the tile totals' block scan gives each tile's first
@@ -2238,7 +2124,6 @@ __device__ __forceinline__ void tiled_plan(uint8_t* lds, const VarGeom& g, const
   }
   if (t <= Gt) tb[t] = before + x - tot;  // tb[Gt] = T
   __syncthreads();
-  NVL_FSTAMP(4);
   T = uniform_u64(T);
   C0 = T * blockIdx.x / gridDim.x;
   C1 = T * (blockIdx.x + 1) / gridDim.x;
@@ -2277,7 +2162,6 @@ __device__ __forceinline__ void tiled_plan(uint8_t* lds, const VarGeom& g, const
     }
   }
   __syncthreads();
-  NVL_FSTAMP(5);
   B0 = long_bufs ? 0 : res[0];
   B1 = long_bufs ? 0 : res[1];
   __syncthreads();  // (the scratch becomes the table image)
@@ -2378,7 +2262,6 @@ __device__ const uint16_t* lpt_order(const VarGeom& g, uint8_t* lds, uint64_t i0
 
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(VarGeom gv, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes > kPermLdsBytes ? kFusedLdsBytes : kPermLdsBytes];
-  NVL_FSTAMP(0);
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1, B0, B1;
   bool long_bufs, multi;
@@ -2388,7 +2271,6 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   // that spills (25 VGPRs, 108 B/lane scratch, cfg3 287 -> 430 us).
   C0 = uniform_u64(C0);
   C1 = uniform_u64(C1);
-  NVL_FSTAMP(1);
   const uint32_t* ubuf = reinterpret_cast<const uint32_t*>(lds + kUnitOff);
   const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,
                        ubuf + kUnitsPerWG, ub0};
@@ -2403,7 +2285,6 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     return;
   }
   run_general<kGenWaves>(g, ka, lds);
-  NVL_FSTAMP(2);
   const Rec* lr = reinterpret_cast<const Rec*>(lds + kRecOff);
   Rec* edge = reinterpret_cast<Rec*>(lds + kEdgeOff);
   uint32_t* last = reinterpret_cast<uint32_t*>(lds + kEdgeOff + 2u * sizeof(Rec));
@@ -2441,7 +2322,6 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     *last = d == gridDim.x - 1 ? 1u : 0u;
   }
   __syncthreads();
-  NVL_FSTAMP(3);
   if (!*last) return;
   // The last workgroup: every edge record (sc1 loads) into the now free table
   // image, then one thread per workgroup whose E_in ends a buffer XORs in the
@@ -2470,7 +2350,6 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
     ka.out[e.buf] = finish(~total, ka.flags);
   }
   if (t == 0) (void)__hip_atomic_exchange((gu32*)ka.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  NVL_FSTAMP(7);
 }
 
 // ReadBlock's trailer checks (table/format.cc:88-135) for blocks whose CRCs
@@ -2636,21 +2515,6 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
 size_t var_recs_bytes(int num_cu) { return 2ull * (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(Rec); }
 size_t var_unit_map_bytes(int num_cu) { return (uint64_t)num_cu * dev::kUnitsPerWG * sizeof(uint64_t); }
 
-#if defined(NVL_DIAG_FUSED)
-extern "C" __attribute__((visibility("default"))) int nvl_diag_fstamps(unsigned long long* host, size_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_fstamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
-#endif
-#if defined(NVL_DIAG_HSTAMPS)
-extern "C" __attribute__((visibility("default"))) int nvl_diag_hstamps(unsigned long long* host, size_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_hstamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
-#endif
-#if defined(NVL_DIAG_STAMPS)
-extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned long long* host, size_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dev::g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 bool var_plan_small(uint64_t n) { return n <= dev::kPlanSmallMax; }
 

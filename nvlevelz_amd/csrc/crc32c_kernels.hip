@@ -312,6 +312,10 @@ struct KArgs {
   uint64_t* tiles = nullptr;
   uint64_t tile_S = 0;  // buffers per tile
   uint32_t tile_G = 0;  // tiles (the head kernel's workgroups)
+  // Head kernel: nonzero allows short mode (every buffer finished in the
+  // head kernel, no body kernel) -- for a fixed batch the host's decision,
+  // for a tiled variable batch per tile, from its scan.
+  uint32_t short_ok = 0;
 };
 
 // floor(a / d) for wave-uniform a < 2^63, d > 0, from a double-precision
@@ -361,6 +365,7 @@ struct FixedGeom {
   // long_heads' raw metadata (offset from base_addr(), length) of buffer i
   __device__ __forceinline__ uint64_t offsets_at(uint64_t i) const { return i * stride; }
   __device__ __forceinline__ uint64_t lengths_at(uint64_t) const { return len; }
+  __device__ __forceinline__ uint32_t lengths_lo(uint64_t) const { return (uint32_t)len; }
   __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   template <bool F = false>
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
@@ -402,6 +407,9 @@ struct VarGeom {
   __device__ __forceinline__ uint64_t total() const { return ldc(chunk_start, n); }
   __device__ __forceinline__ uint64_t offsets_at(uint64_t i) const { return offsets[i]; }
   __device__ __forceinline__ uint64_t lengths_at(uint64_t i) const { return lengths[i]; }
+  __device__ __forceinline__ uint32_t lengths_lo(uint64_t i) const {  // (little-endian low word)
+    return reinterpret_cast<const uint32_t*>(lengths)[2 * i];
+  }
   __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
     uint64_t lo = 0, hi = n;  // invariant: chunk_start[lo] <= t < chunk_start[hi]
@@ -805,6 +813,11 @@ __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane) {
 #define NVL_STAMP1() do {} while (0)
 #define NVL_COUNT() do {} while (0)
 #define NVL_STAMP_END() do {} while (0)
+#endif
+#ifndef NVL_TL_DECL  // phase timeline (same header): NVL_TL(k) at phase boundaries
+#define NVL_TL_DECL() do {} while (0)
+#define NVL_TL(k) do {} while (0)
+#define NVL_TL_END() do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1483,7 +1496,7 @@ __device__ bool tile_scan(const G& g, const KArgs& ka, uint8_t* lds) {
 #pragma unroll
     for (uint32_t v = 0; v < (uint32_t)NW; ++v) m = max(m, wmax[v]);
     ka.tiles[2ull * blockIdx.x] = carry;
-    ka.tiles[2ull * blockIdx.x + 1] = m;
+    ka.tiles[2ull * blockIdx.x + 1] = max(m, 3u);  // head mode: the body kernel has work (> 2, see run_heads)
   }
   __syncthreads();  // (the scratch becomes the table image)
   return need;
@@ -1502,136 +1515,243 @@ __device__ __forceinline__ uint32_t bitwise_raw(const uint8_t* p, uint32_t n, ui
   return l;
 }
 
-// Head kernel LDS beyond the table image: the long-head list of a sub-range
-// (u32 size, u32 drained, u16 index[kHeadSub]).
+// Head kernel LDS beyond the table image: a sub-range's work list and the
+// fused tile scan's scratch.
+//   u32 ctl[4]: [0] list A size, [1] slots handed out, [2] list B size
+//   u16 list[kHeadSub]: list A (one pass per entry) from the front, list B
+//       (two passes per entry) from the back, as indices within the sub-range
+//   u64 wsum[16], u32 wmax[16]: per-wave scan totals / largest chunk counts
 constexpr uint64_t kHeadSub = (uint64_t)kWave * kWavesPerWG;  // buffers per sub-range: <= 64 per wave
 constexpr uint32_t kLongOff = kLdsBytes;
-constexpr uint32_t kHeadLdsBytes = kLongOff + 8u + 2u * (uint32_t)kHeadSub;
-static_assert(kLongOff % 16u == 0u && kHeadLdsBytes <= 160u * 1024u, "head kernel LDS exceeds 160 KiB");
-constexpr uint32_t kLongOk = 1u << 16, kLongLast = 1u << 17;  // long-head tags: index within the sub-range | flags
+constexpr uint32_t kListOff = kLongOff + 16u;
+constexpr uint32_t kScanOff = kListOff + 2u * (uint32_t)kHeadSub;
+constexpr uint32_t kHeadLdsBytes = kScanOff + 16u * (8u + 4u);
+static_assert(kLongOff % 16u == 0u && kScanOff % 8u == 0u && kHeadLdsBytes <= 160u * 1024u,
+              "head kernel LDS exceeds 160 KiB");
 
-// Long heads of a sub-range (its LDS list), two per pass with interleaved
-// chains, pulled from the list by every wave of the workgroup.  A head is a
-// whole chunk [ce - 4096, ce) with its bytes before p masked (load_general /
-// realign_general with hd).  Pipeline: a pass builds the words of the pair in
-// hand (waiting for their loads), turns the next pair's metadata -- loaded a
-// pass earlier, before those chunk loads -- into positions, pulls the pair
-// after it and issues its metadata loads, issues the next pair's chunk loads,
-// then runs the chains.  Past the end of the list a slot is a dummy chunk in
-// the table blob (loaded, not written; a pair of two dummies is not run).
+// Work-list entries (u16): index within the sub-range (bits 0..9) | kLOut
+// when the entry is a whole buffer (J == 1).
+constexpr uint32_t kLOut = 1u << 15;
+static_assert(kHeadSub <= 1024u, "list entries hold a 10-bit index");
+
+// Drain pass tags: list entry (bits 0..15) | flags.
+constexpr uint32_t kTOk = 1u << 16;    // a real pass
+constexpr uint32_t kTOut = 1u << 17;   // the whole buffer (J == 1): out[i] = finish(~raw)
+constexpr uint32_t kTHc = 1u << 18;    // head mode: the head of a longer buffer, hc[i] = raw
+constexpr uint32_t kTInj = 1u << 19;   // short mode: a J == 2 buffer's body, its head's register from hc[i]
+constexpr uint32_t kTTiny = 1u << 20;  // (kTInj) a 1..3-byte head: hc[i] is rewritten for the body kernel
+constexpr uint32_t kTPair = 1u << 21;  // short mode: a slot holding the head and the body of one J == 2 buffer
+
+// One pass of the drain (wave-uniform): the chunk [ce - 4096, ce) with its
+// bytes before ps zeroed and sx XORed into the 4 bytes at ps.  The body pass
+// of a two-chunk buffer in list A (kTInj) starts from its head's register
+// instead: raw(s, H || B) = raw(raw(s, H), B) = raw(0, B ^ raw(s, H))
+// (crc32c_math.h), so raw(s, H) is XORed into the body's first word and the
+// pass yields the whole buffer -- no shift, no combine.  raw(s, H) is in
+// hc[i] before the drain starts: a 1..3-byte head fed bitwise by its lane
+// at classification, a head that starts a page's first granule (which a
+// masked pass cannot read: load_general) by a pre-drain lane-group round.
+struct SlotPass {
+  uintptr_t ce, ps;
+  uint32_t sx, tag;
+};
+
+// The drain of a sub-range's lists, two passes per step with interleaved
+// chains, every wave of the workgroup pulling slots from one LDS counter.
+// Slot k < nB is list B's k-th entry (a J == 2 buffer: its head and body);
+// later slots hold two list-A entries each.  Pipeline: a step builds the
+// words of the slot in hand (waiting for its loads), turns the next slot's
+// metadata -- loaded a step earlier, before those chunk loads -- into
+// positions, pulls the slot after it and issues its metadata loads, issues
+// the next slot's chunk loads, then runs the chains.  Past the end a pass is
+// a dummy chunk in the table blob (loaded, not written; a slot of two
+// dummies is not run).  The metadata is the offset, the length's low word
+// (list entries have at most two chunks or are heads: h = ((L - 1) & 4095)
+// + 1, J == 1 from the entry's kLOut) and ~init: the fewer registers the
+// next slot's loads hold, the more LDS lookups of the chains the compiler
+// keeps in flight.
 template <class G>
-__device__ __forceinline__ void long_heads(const G& g, const KArgs& ka, uint8_t* lds, const LaneBase& lb,
-                                           uint64_t sub0, uint32_t* lcnt, const uint16_t* llist) {
+__device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t* lds, const LaneBase& lb,
+                                           uint64_t sub0, uint32_t* ctl, const uint16_t* list, bool shortm) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nl = uniform_u32(lcnt[0]);
-  if (nl == 0) return;
+  const uint32_t nA = uniform_u32(ctl[0]), nB = uniform_u32(ctl[2]);
+  const uint32_t nslots = nB + (nA + 1u) / 2u;
+  if (nslots == 0) return;
   const uintptr_t safe = (uintptr_t)ka.tables;
   const uint32_t* const ibase = g.init ? g.init : reinterpret_cast<const uint32_t*>(safe);
   auto pull = [&]() -> uint32_t {
     uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(&lcnt[1], 2u);
+    if (lane == 0) v = atomicAdd(&ctl[1], 1u);
     return uniform_u32(v);
   };
-  // metadata of list entries k, k+1 (raw loads; all lanes the same address)
+  // metadata of slot k's entries (raw loads, all lanes the same address)
+  uint64_t mo0, mo1;
+  uint32_t mL0, mL1, mi0, mi1, mj0, mj1;
+  auto meta = [&](uint32_t k) {
+    const bool isb = k < nB;
+    const uint32_t a = 2u * (k - nB);
+    mj0 = isb ? ((uint32_t)list[kHeadSub - 1u - k] | kTOk | kTPair) : (a < nA ? (uint32_t)list[a] | kTOk : 0u);
+    mj1 = isb ? mj0 : (a + 1u < nA ? (uint32_t)list[a + 1u] | kTOk : 0u);
+    const uint64_t i0 = sub0 + (mj0 & 1023u), i1 = sub0 + (mj1 & 1023u);
+    mo0 = g.offsets_at(i0);
+    mL0 = g.lengths_lo(i0);
+    mi0 = ibase[g.init ? i0 : 0u];
+    mo1 = g.offsets_at(i1);
+    mL1 = g.lengths_lo(i1);
+    mi1 = ibase[g.init ? i1 : 0u];
+  };
+  // positions of one entry (uniform: lane 0's copy); for a PAIR slot the
+  // first pass is the head, the second the body
+  auto pos = [&](uint64_t mo, uint32_t mL, uint32_t mi, uint32_t mj, bool second, SlotPass& q) {
+    const uint32_t tag = uniform_u32(mj);
+    const uint32_t L = uniform_u32(mL);  // (low word: see above)
+    const uint32_t h = ((L - 1u) & (kChunk - 1u)) + 1u;
+    const uintptr_t p = g.base_addr() + uniform_u64(mo);
+    const uint32_t s = ~(g.init ? uniform_u32(mi) : g.init_all);
+    q.tag = tag;
+    if (!(tag & kTOk)) {
+      q.ce = safe + kChunk;
+      q.ps = safe;
+      q.sx = 0u;
+      q.tag = 0u;
+    } else if (tag & kTPair) {
+      q.ce = second ? p + L : p + h;
+      q.ps = second ? p + h : p;
+      q.sx = second ? 0u : s;
+    } else if (tag & kLOut) {
+      q.ce = p + L;
+      q.ps = p;
+      q.sx = s;
+      q.tag |= kTOut;
+    } else if (shortm) {  // J == 2: the body, from its head's register (hc[i])
+      q.ce = p + L;
+      q.ps = q.ce - kChunk;
+      q.sx = h < 4u ? s >> (8u * h) : 0u;  // (kTTiny: hc[i]'s rewrite for the body kernel)
+      q.tag |= kTInj | (h < 4u ? kTTiny : 0u);
+    } else {  // head mode: a long head
+      q.ce = p + h;
+      q.ps = p;
+      q.sx = s;
+      q.tag |= kTHc;
+    }
+  };
+  auto aux_load = [&](const SlotPass& q) -> uint32_t {  // hc[i] of a kTInj pass (bypassing L1)
+    const uintptr_t a = (q.tag & kTInj) ? (uintptr_t)(ka.hc + sub0 + (q.tag & 1023u)) : safe;
+    return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)a);
+  };
   uint32_t k = pull();
-  uint64_t mo0, mL0, mo1, mL1;
-  uint32_t mi0, mi1, mj0, mj1;
-#define NVL_META(K)                                                                                    \
-  do {                                                                                                 \
-    mj0 = (K) < nl ? (uint32_t)llist[(K)] | kLongOk : 0u;                                              \
-    mj1 = (K) + 1u < nl ? (uint32_t)llist[(K) + 1u] | kLongOk : 0u;                                    \
-    const uint64_t i0_ = sub0 + (mj0 & 0xFFFFu), i1_ = sub0 + (mj1 & 0xFFFFu);                         \
-    mo0 = g.offsets_at(i0_);                                                                           \
-    mL0 = g.lengths_at(i0_);                                                                           \
-    mi0 = ibase[g.init ? i0_ : 0u];                                                                    \
-    mo1 = g.offsets_at(i1_);                                                                           \
-    mL1 = g.lengths_at(i1_);                                                                           \
-    mi1 = ibase[g.init ? i1_ : 0u];                                                                    \
-  } while (0)
-  // a position from loaded metadata (uniform: lane 0's copy)
-#define NVL_POS(MO, ML, MI, MJ, CE, P, S, TAG)                                                          \
-  do {                                                                                                 \
-    TAG = uniform_u32((uint32_t)(MJ));                                                                 \
-    const uint64_t L_ = uniform_u64(ML);                                                               \
-    const uint32_t J_ = chunks_for(L_);                                                                \
-    P = (TAG & kLongOk) ? g.base_addr() + uniform_u64(MO) : safe + 16u;                                 \
-    CE = (TAG & kLongOk) ? P + head_bytes(L_, J_) : safe + kChunk;                                     \
-    S = ~(g.init ? uniform_u32(MI) : g.init_all);                                                      \
-    TAG |= (J_ == 1u) ? kLongLast : 0u;                                                                \
-  } while (0)
-#define NVL_WRITE(TAG, RAW)                                                                            \
-  do {                                                                                                 \
-    if (((TAG) & kLongOk) && lane == 0) {                                                              \
-      const uint64_t ib_ = sub0 + ((TAG) & 0xFFFFu);                                                   \
-      if ((TAG) & kLongLast) ka.out[ib_] = finish(~(RAW), ka.flags);                                   \
-      else ka.hc[ib_] = (RAW);                                                                         \
-    }                                                                                                  \
-  } while (0)
-  NVL_META(k);
-  uintptr_t ceA, pA, ceB, pB;
-  uint32_t sA, tA, sB, tB;
-  NVL_POS(mo0, mL0, mi0, mj0, ceA, pA, sA, tA);
-  NVL_POS(mo1, mL1, mi1, mj1, ceB, pB, sB, tB);
+  meta(k);
+  SlotPass A, B;
+  pos(mo0, mL0, mi0, mj0, false, A);
+  pos(mo1, mL1, mi1, mj1, true, B);
   k = pull();
-  NVL_META(k);
+  meta(k);
   Chunk cA, cB;
-  load_general(ceA, true, pA, lane, cA);
-  load_general(ceB, true, pB, lane, cB);
+  load_general(A.ce, true, A.ps, lane, cA);
+  load_general(B.ce, true, B.ps, lane, cB);
+  uint32_t xA = aux_load(A), xB = aux_load(B);
   while (true) {
-    // a pair wholly past the list's end is not run (its loads, of the table
-    // blob, just drain)
-    if (!(tA & kLongOk)) break;
+    if (!(A.tag & kTOk)) break;  // (a slot wholly past the end: its loads just drain)
     uint32_t w[2][16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[0][q] = cA.d[q];
     row_transpose(w[0]);
-    realign_general(ceA, true, pA, sA, lane, cA, w[0]);
+    realign_general(A.ce, true, A.ps, (A.tag & kTInj) ? 0u : A.sx, lane, cA, w[0]);
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[1][q] = cB.d[q];
     row_transpose(w[1]);
-    realign_general(ceB, true, pB, sB, lane, cB, w[1]);
-    const uint32_t uA = tA, uB = tB;
-    NVL_POS(mo0, mL0, mi0, mj0, ceA, pA, sA, tA);
-    NVL_POS(mo1, mL1, mi1, mj1, ceB, pB, sB, tB);
+    realign_general(B.ce, true, B.ps, (B.tag & kTInj) ? 0u : B.sx, lane, cB, w[1]);
+    // a kTInj body starts from its head's register (word 0 of lane 0)
+    const uint32_t iA = (A.tag & kTInj) ? xA : 0u, iB = (B.tag & kTInj) ? xB : 0u;
+    if (lane == 0) {
+      w[0][0] ^= iA;
+      w[1][0] ^= iB;
+    }
+    // hc of a 1..3-byte head in the body kernel's convention (raw(s, H) ^
+    // (s >> 8h): that kernel injects s >> 8h into the body itself), for a
+    // mixed batch whose body kernel re-runs this tile's two-chunk bodies
+    const uint32_t hcA = iA ^ A.sx, hcB = iB ^ B.sx;
+    const uint32_t uA = A.tag, uB = B.tag;
+    pos(mo0, mL0, mi0, mj0, false, A);
+    pos(mo1, mL1, mi1, mj1, true, B);
     k = pull();
-    NVL_META(k);
-    load_general(ceA, true, pA, lane, cA);
-    load_general(ceB, true, pB, lane, cB);
+    meta(k);
+    load_general(A.ce, true, A.ps, lane, cA);
+    load_general(B.ce, true, B.ps, lane, cB);
+    xA = aux_load(A);
+    xB = aux_load(B);
     uint32_t raws[2];
     chains<2, false>(lds, lb, w, lane, raws);
-    NVL_WRITE(uA, raws[0]);
-    NVL_WRITE(uB, raws[1]);
-    if (!(uB & kLongOk)) break;  // (entries are drained in order per wave: uA empty implies uB empty)
+    // shift4096 spreads its lookups over the lanes of a quad: every lane runs it
+    const uint32_t shA = (uA & kTPair) ? shift4096(lds, raws[0], lane) : 0u;
+    if (lane == 0) {
+      const uint64_t ia = sub0 + (uA & 1023u), ib = sub0 + (uB & 1023u);
+      if (uA & kTPair) {  // head + body of one buffer
+        ka.out[ia] = finish(~(shA ^ raws[1]), ka.flags);
+        if (ka.hc) ka.hc[ia] = raws[0];
+      } else {
+        if (uA & (kTOut | kTInj)) ka.out[ia] = finish(~raws[0], ka.flags);
+        if (uA & (kTHc | kTTiny)) ka.hc[ia] = (uA & kTHc) ? raws[0] : hcA;
+        if (uB & (kTOut | kTInj)) ka.out[ib] = finish(~raws[1], ka.flags);
+        if (uB & (kTHc | kTTiny)) ka.hc[ib] = (uB & kTHc) ? raws[1] : hcB;
+      }
+    }
+    if (!(uB & kTOk)) break;  // (slots are handed out in order: a half-empty one is the last)
   }
-#undef NVL_WRITE
-#undef NVL_POS
-#undef NVL_META
 }
 
+// The head kernel: a workgroup takes its buffers (its plan tile when the
+// batch is variable-length) in sub-ranges of kHeadSub, a slice of at most 64
+// buffers (one per lane) per wave.
+//   head mode: the partial first chunks ("heads") of the buffers -- a
+//     one-chunk buffer is finished (out[i]), a longer one leaves hc[i] for
+//     the body kernel; buffers of < 4 bytes and 1..3-byte heads bitwise,
+//     heads of <= 1024 bytes in the wave's own lane-group rounds, longer
+//     ones as whole masked chunks from the workgroup's LDS list.
+//   short mode (every buffer of the tile has at most 2 chunks, and none
+//     needs a page-start masked head: KArgs::short_ok and the tile's scan):
+//     EVERY buffer is finished here, so the body kernel has nothing left --
+//     one-chunk buffers of > 1024 bytes as one pass (list A), two-chunk
+//     buffers as head + body passes in one slot (list B) or, with a 1..3-byte
+//     head, as the body pass with the head folded in inline (list A); the
+//     rest in lane-group rounds.  tiles[2b+1] (the tile's largest chunk
+//     count) stays <= 2 only for a short-mode tile: the body kernel exits at
+//     once when every tile is one.
+// After the lists are complete each wave runs its own rounds and then joins
+// the drain, so a wave with many rounds leaves the list to the others (a
+// barrier between rounds and drain made the whole workgroup wait for its
+// slowest wave's rounds: up to 13 us on 10^5 buffers of 3364..4109 B).
 template <class G>
 __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* lds) {
+  NVL_TL_DECL();
+  NVL_TL(0);
   const int lane = threadIdx.x & 63;
   const uint32_t wv = uniform_u32(threadIdx.x >> 6);
   // the workgroup's buffers: its plan tile when there is one
   uint64_t w0 = g.n * blockIdx.x / gridDim.x, w1 = g.n * (blockIdx.x + 1) / gridDim.x;
-  bool tables = true;
+  bool tiled = false;
   if constexpr (G::kTiled) {
     if (ka.lpre) {
-      tables = tile_scan<kWavesPerWG>(g, ka, lds);
+      tiled = true;
       w0 = min(g.n, ka.tile_S * blockIdx.x);
       w1 = min(g.n, w0 + ka.tile_S);
     }
   }
-  // The workgroup's buffers go in sub-ranges of kHeadSub, a slice of at most
-  // 64 buffers (one per lane) per wave.  Short heads run in the wave's own lane-group rounds; long
-  // heads are appended to an LDS list that all waves then drain two at a
-  // time (long_heads): with a static per-wave split the waves' long-head
-  // time ranged 36..96 us for equal work (issue arbitration favours older
-  // waves; tools/diag/hstamps.py).
+  // one sub-range tiles fold their plan scan into the classification pass
+  const bool fused_scan = tiled && w1 - w0 <= kHeadSub;
+  bool shortm = !tiled && ka.short_ok != 0u;
+  if constexpr (G::kTiled) {
+    if (tiled && !fused_scan) {
+      (void)tile_scan<kWavesPerWG>(g, ka, lds);  // head mode (large tiles)
+      NVL_TL(1);
+    }
+  }
   const LaneBase lb = make_lane_base(lane);
-  uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds + kLongOff);  // [0] list size, [1] drained
-  uint16_t* llist = reinterpret_cast<uint16_t*>(lds + kLongOff + 8u);
-  uintptr_t lp = 0;  // the lane's buffer of the current group: start, length, ~init
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(lds + kLongOff);
+  uint16_t* list = reinterpret_cast<uint16_t*>(lds + kListOff);
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(lds + kScanOff);
+  uint32_t* wmax = reinterpret_cast<uint32_t*>(lds + kScanOff + 16u * 8u);
+  uintptr_t lp = 0;  // the lane's buffer of the current sub-range: start, length, ~init
   uint64_t lL = 0;
   uint32_t ls = 0;
   // the wave's slice of a sub-range [s0, s1): at most 64 buffers
@@ -1644,11 +1764,56 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     slice(w0, min(w1, w0 + kHeadSub), a, b);
     if (a + (uint64_t)lane < b) g.lane_meta(a + (uint64_t)lane, lp, lL, ls);  // in flight during the fill
   }
-  if (threadIdx.x < 2) lcnt[threadIdx.x] = 0u;
-  if (tables) {
-    fill_lds<kWavesPerWG>(lds, ka.tables);
-    __syncthreads();
-  }
+  if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
+  fill_lds<kWavesPerWG>(lds, ka.tables);
+  if (!fused_scan) __syncthreads();
+  NVL_TL(2);
+  if (fused_scan) {  // (the first -- and only -- sub-range's lanes hold their metadata)
+    uint64_t gb, ge;
+    slice(w0, w1, gb, ge);
+    const bool valid = gb + (uint64_t)lane < ge;
+    const uint64_t i = gb + (uint64_t)lane;
+    const bool tiny = valid && lL < 4;
+    const uint32_t J = valid ? chunks_for(lL) : 0u;
+    const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);
+    const bool pstart = ((lp >> 4) & 255u) == 0u;
+      // the tile's plan (tile_scan's lpre / tiles) from the lanes' lengths:
+      // the waves' slices are consecutive, so one wave scan + one barrier
+      uint64_t x = J;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+      }
+      uint32_t mj = J;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mj = max(mj, (uint32_t)__shfl_xor((int)mj, o));
+      if (lane == 63) wsum[wv] = x;
+      if (lane == 0) wmax[wv] = mj;
+      __syncthreads();  // (also: the tables are in LDS)
+      // the 16 waves' totals and flags across lanes 0..15 (a wave scan, not
+      // 48 LDS reads held in registers at once)
+      const bool lw = (uint32_t)lane < kWavesPerWG;
+      const uint64_t sv = lw ? wsum[lane] : 0;
+      uint32_t mv = lw ? wmax[lane] : 0u;
+      uint64_t inc = sv;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const uint64_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+        mv = max(mv, (uint32_t)__shfl_xor((int)mv, o));
+      }
+      const uint64_t tot = lane_u64(inc, kWavesPerWG - 1u);
+      const uint64_t before = lane_u64(inc - sv, wv);
+      const uint32_t m = lane_u32(mv, 0u);
+      shortm = ka.short_ok != 0u && m <= 2u;
+      if (valid) ka.lpre[i] = before + x - J;
+      if (threadIdx.x == 0) {
+        ka.tiles[2ull * blockIdx.x] = tot;
+        ka.tiles[2ull * blockIdx.x + 1] = shortm ? m : max(m, 3u);  // > 2: the body kernel has work
+      }
+      NVL_TL(1);
+    }
   for (uint64_t sub0 = w0; sub0 < w1; sub0 += kHeadSub) {  // (workgroup-uniform trip count)
     const uint64_t sub1 = min(w1, sub0 + kHeadSub);
     uint64_t gb, ge;
@@ -1662,39 +1827,65 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       if (valid) g.lane_meta(i, lp, lL, ls);
     }
     const bool tiny = valid && lL < 4;
-    const uint32_t J = chunks_for(lL);
-    const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);  // first chunk's bytes
-    const bool shrt = valid && !tiny && hl < 4;               // 1..3-byte head of a longer buffer
-    const bool head = valid && !tiny && !shrt && hl < kChunk;
+    const uint32_t J = valid ? chunks_for(lL) : 0u;
+    const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);  // first chunk's bytes (when valid)
+    const bool pstart = ((lp >> 4) & 255u) == 0u;          // p in a 4 KiB page's first 16 bytes
     const uint32_t cls = hl <= 64u ? 0u : (hl <= 256u ? 1u : (hl <= 1024u ? 2u : 3u));
+    bool inA, inB, round, shrt, pre = false;
+    if (shortm) {  // (workgroup-uniform)
+      // a two-chunk buffer whose 4..4095-byte head starts a page's first
+      // granule: the head in a round before the drain (a masked pass would
+      // read below the page), its register handed to the body pass via hc
+      pre = valid && !tiny && J == 2u && hl >= 4u && hl < kChunk && pstart;
+      inA = valid && !tiny && ((J == 1u && hl > 1024u && (hl == kChunk || !pstart)) || (J == 2u && (hl < 4u || pre)));
+      inB = valid && !tiny && J == 2u && hl >= 4u && !pre;
+      round = valid && !tiny && J == 1u && !inA;
+      shrt = false;
+    } else {
+      shrt = valid && !tiny && hl < 4;  // 1..3-byte head of a longer buffer
+      const bool head = valid && !tiny && !shrt && hl < kChunk;
+      // Long heads (1025..4095 bytes) run as whole masked chunks from the
+      // list (as P = 64 lane-group rounds, whose 64-byte-per-lane loads touch
+      // 32 lines per instruction, this class ran at ~2.7 TB/s), except where
+      // the buffer starts in a page's first 16 bytes (load_general reads up to
+      // 12 bytes below p's granule).
+      inA = head && cls == 3u && !pstart;
+      inB = false;
+      round = head && !inA;
+    }
     // what setup pulls across lanes: head bytes (< 4096) | kHeadLast << 16
     const uint32_t hlx = (uint32_t)(hl & 0xFFFFu) | (J == 1u ? kHeadLast << 16 : 0u);
     if (tiny) ka.out[i] = finish(~bitwise_raw(reinterpret_cast<const uint8_t*>(lp), (uint32_t)lL, ls), ka.flags);
     // hc = raw(0, head ^ s's low bytes) = raw(s, head) ^ (s >> 8 hl): the body
     // injects s's remaining bytes into its first word itself
     if (shrt) ka.hc[i] = bitwise_raw(reinterpret_cast<const uint8_t*>(lp), (uint32_t)hl, ls) ^ (ls >> (8u * (uint32_t)hl));
-    // Long heads (1025..4095 bytes) run as whole chunks with the body
-    // kernels' coalesced row loads and transpose (long_heads): as P = 64
-    // lane-group rounds, whose 64-byte-per-lane loads touch 32 lines per
-    // instruction, this class ran at ~2.7 TB/s.  A head whose buffer starts
-    // in the first 16 bytes of a 4 KiB page stays in the rounds (load_general
-    // reads up to 12 bytes below p's granule).
-    const bool coal = head && cls == 3u && ((lp >> 4) & 255u) != 0u;  // (load_general: g not a page start)
-    {
-      const uint64_t mco = __ballot(coal);
-      if (mco) {  // append to the workgroup's list (index within the sub-range)
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&lcnt[0], (uint32_t)__builtin_popcountll(mco));
-        base = uniform_u32(base);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mco >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mco, 0u));
-        if (coal) llist[base + rank] = (uint16_t)(i - sub0);
+    // short mode: a 1..3-byte head's register raw(s, H) for its body pass
+    // (list A, kTInj), stored before the lists-complete barrier
+    if (shortm && valid && !tiny && J == 2u && hl < 4u)
+      ka.hc[i] = bitwise_raw(reinterpret_cast<const uint8_t*>(lp), (uint32_t)hl, ls);
+    {  // append to the workgroup's lists (index within the sub-range)
+      const uint64_t ma = __ballot(inA), mb = __ballot(inB);
+      const uint32_t rank_a = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+      const uint32_t rank_b = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+      uint32_t ba = 0, bb = 0;
+      if (lane == 0) {
+        if (ma) ba = atomicAdd(&ctl[0], (uint32_t)__builtin_popcountll(ma));
+        if (mb) bb = atomicAdd(&ctl[2], (uint32_t)__builtin_popcountll(mb));
       }
+      ba = uniform_u32(ba);
+      bb = uniform_u32(bb);
+      if (inA) list[ba + rank_a] = (uint16_t)((uint32_t)(i - sub0) | (J == 1u ? kLOut : 0u));
+      if (inB) list[kHeadSub - 1u - (bb + rank_b)] = (uint16_t)(i - sub0);
     }
     uint64_t m[4];
     uint32_t nr[4], NR = 0;
+    // phase 0: the pre-drain heads (short mode); then the lists are complete;
+    // phase 1: the wave's own rounds
+    for (int ph = 0; ph < 2; ++ph) {  // (workgroup-uniform)
+    NR = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      m[c] = __ballot(head && !coal && cls == (uint32_t)c);
+      m[c] = __ballot((ph == 0 ? pre : round) && cls == (uint32_t)c);
       const uint32_t per = 64u >> (2 * c);
       nr[c] = ((uint32_t)__builtin_popcountll(m[c]) + per - 1u) / per;
       NR += nr[c];
@@ -1771,16 +1962,24 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       asm volatile("" ::: "memory");
       finish_round(head_chain(lds, lb, w, nl, lane), tag, P);
     }
-    // (the last reloads drain before the next group's buffers are set up)
+    // (the last reloads drain before the list's first loads are issued)
     }
-    if (tables) {  // (workgroup-uniform)
-      __syncthreads();  // the list is complete
-      long_heads(g, ka, lds, lb, sub0, lcnt, llist);
-      __syncthreads();  // drained
-      if (threadIdx.x < 2) lcnt[threadIdx.x] = 0u;
+    if (ph == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the hc stores (pre-drain rounds, 1..3-byte heads) done
+      __syncthreads();  // the lists are complete (and the tables in LDS)
+      NVL_TL(3);
+    }
+    }
+    NVL_TL(4);
+    drain_list(g, ka, lds, lb, sub0, ctl, list, shortm);
+    NVL_TL(5);
+    if (sub0 + kHeadSub < w1) {  // (workgroup-uniform) the lists are reused by the next sub-range
+      __syncthreads();
+      if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
       __syncthreads();
     }
   }
+  NVL_TL_END();
 }
 
 template <class G>
@@ -2266,6 +2465,9 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   uint64_t C0, C1, B0, B1;
   bool long_bufs, multi;
   tiled_plan<kGenWaves>(lds, gv, ka, C0, C1, long_bufs, B0, B1, multi);
+  // Every tile's largest chunk count <= 2: the head kernel ran each tile in
+  // short mode and finished every buffer (run_heads) -- nothing left here.
+  if (!multi) return;
   // The range is uniform, but the 64-bit divisions that made it ran on the
   // VALU: pin it to SGPRs, or it stays in VGPRs through the main loop and
   // that spills (25 VGPRs, 108 B/lane scratch, cfg3 287 -> 430 us).
@@ -2436,18 +2638,20 @@ static inline uint32_t head_grid(int num_cu, uint64_t n) {
 
 template <class G>
 static hipError_t launch_heads(const LaunchCtx& lc, const G& g, uint32_t* out, uint32_t flags, uint32_t* hc,
-                               hipEvent_t ev_start, uint64_t* lpre = nullptr, uint64_t* tiles = nullptr) {
+                               hipEvent_t ev_start, uint64_t* lpre = nullptr, uint64_t* tiles = nullptr,
+                               bool short_ok = false, hipEvent_t ev_stop = nullptr) {
   const uint32_t grid = head_grid(lc.num_cu, g.n);
   dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, hc};
+  ka.short_ok = short_ok ? 1u : 0u;
   if (lpre) {  // tiles of the variable-length plan: one per workgroup
     ka.lpre = lpre;
     ka.tiles = tiles;
     ka.tile_G = grid;
     ka.tile_S = (g.n + grid - 1) / grid;
   }
-  if (ev_start)
+  if (ev_start || ev_stop)
     hipExtLaunchKernelGGL(dev::crc32c_head_kernel<G>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, ev_start,
-                          nullptr, 0u, g, ka);
+                          ev_stop, 0u, g, ka);
   else
     hipLaunchKernelGGL(dev::crc32c_head_kernel<G>, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
   return hipGetLastError();
@@ -2474,20 +2678,21 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
   Rec* recs = J > 1 ? ws : nullptr;
   const bool heads = !aligned && dev::head_first(len);  // every buffer's first chunk is a head chunk
-  const bool body = !(heads && J == 1);                 // some buffer has a full chunk
+  // Short mode (run_heads): two-chunk buffers with a 1..3-byte head (block |
+  // type of 4096-byte blocks at a fixed stride) are finished by the head
+  // kernel, body chunk and all; no masked head can start a page there.
+  const bool short_all = heads && J == 2 && dev::head_bytes(len, J) < 4u;
+  const bool body = !(heads && (J == 1 || short_all));  // some buffer has a chunk left for a body kernel
   uint32_t* hc = heads && J > 1
                      ? reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws) +
                                                    (recs_part(lc.num_cu, len, n) + 255) / 256 * 256)
                      : nullptr;
   hipEvent_t ev_start = lc.ev_start;
   if (heads) {
-    hipError_t eh = launch_heads(lc, g, out, flags, hc, ev_start);
-    if (eh != hipSuccess) return eh;
+    hipError_t eh = launch_heads(lc, g, out, flags, hc, ev_start, nullptr, nullptr, short_all,
+                                 body ? nullptr : lc.ev_stop);
+    if (eh != hipSuccess || !body) return eh;
     ev_start = nullptr;
-    if (!body) {
-      if (lc.ev_stop) return hipEventRecord(lc.ev_stop, lc.stream);
-      return hipSuccess;
-    }
   }
   dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc};
   hipEvent_t stop_main = J == 1 ? lc.ev_stop : nullptr;  // else the fix-up records it
@@ -2524,7 +2729,7 @@ hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint
   if (n == 0) return hipSuccess;
   if (!lc.counter || !lpre || !tiles || lc.num_cu > (int)dev::kMaxTiles) return hipErrorInvalidValue;
   dev::VarGeom g{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
-  hipError_t eh = launch_heads(lc, g, out, flags, hc, nullptr, lpre, tiles);
+  hipError_t eh = launch_heads(lc, g, out, flags, hc, nullptr, lpre, tiles, /*short_ok=*/true);
   if (eh != hipSuccess) return eh;
   dev::KArgs ka{out, flags, recs, lc.tables, lc.counter, hc};
   ka.lpre = lpre;

@@ -37,3 +37,27 @@ extern "C" __attribute__((visibility("default"))) int nvl_diag_stamps(unsigned l
              ? 0
              : -1;
 }
+
+// Multi-point timeline (up to 8 stamps per wave) for kernels with phases:
+// NVL_TL_DECL() at entry, NVL_TL(k) at phase boundaries, NVL_TL_END() at
+// exit; read back with nvl_diag_tl() (tools/diag/tl.py).
+namespace nvl {
+namespace dev {
+__device__ unsigned long long g_tl[8 * 65536];
+}
+}  // namespace nvl
+#define NVL_TL_DECL() unsigned long long tl_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define NVL_TL(k) (tl_[(k)] = __builtin_amdgcn_s_memrealtime())
+#define NVL_TL_END()                                                                        \
+  do {                                                                                      \
+    const uint32_t wave_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);              \
+    if ((threadIdx.x & 63) == 0 && wave_ < 65536) {                                         \
+      tl_[7] = __builtin_amdgcn_s_memrealtime();                                            \
+      for (int k_ = 0; k_ < 8; ++k_) ::nvl::dev::g_tl[8 * wave_ + k_] = tl_[k_];            \
+    }                                                                                       \
+  } while (0)
+
+extern "C" __attribute__((visibility("default"))) int nvl_diag_tl(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(::nvl::dev::g_tl), n * sizeof(unsigned long long)) == hipSuccess ? 0
+                                                                                                               : -1;
+}

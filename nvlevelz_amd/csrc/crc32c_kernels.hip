@@ -366,6 +366,12 @@ struct FixedGeom {
   __device__ __forceinline__ uint64_t offsets_at(uint64_t i) const { return i * stride; }
   __device__ __forceinline__ uint64_t lengths_at(uint64_t) const { return len; }
   __device__ __forceinline__ uint32_t lengths_lo(uint64_t) const { return (uint32_t)len; }
+  // buffer i's offset from base_addr(), length's low word and ~init, wave-uniform (scalar loads)
+  __device__ __forceinline__ void meta_s(uint64_t i, uint64_t& o, uint32_t& Llo, uint32_t& s) const {
+    o = i * stride;
+    Llo = (uint32_t)len;
+    s = ~(init ? ldc(init, i) : init_all);
+  }
   __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   template <bool F = false>
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
@@ -409,6 +415,11 @@ struct VarGeom {
   __device__ __forceinline__ uint64_t lengths_at(uint64_t i) const { return lengths[i]; }
   __device__ __forceinline__ uint32_t lengths_lo(uint64_t i) const {  // (little-endian low word)
     return reinterpret_cast<const uint32_t*>(lengths)[2 * i];
+  }
+  __device__ __forceinline__ void meta_s(uint64_t i, uint64_t& o, uint32_t& Llo, uint32_t& s) const {
+    o = ldc(offsets, i);
+    Llo = ldc(reinterpret_cast<const uint32_t*>(lengths), 2 * i);
+    s = ~(init ? ldc(init, i) : init_all);
   }
   __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
@@ -1578,36 +1589,32 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
   const uint32_t nslots = nB + (nA + 1u) / 2u;
   if (nslots == 0) return;
   const uintptr_t safe = (uintptr_t)ka.tables;
-  const uint32_t* const ibase = g.init ? g.init : reinterpret_cast<const uint32_t*>(safe);
   auto pull = [&]() -> uint32_t {
     uint32_t v = 0;
     if (lane == 0) v = atomicAdd(&ctl[1], 1u);
     return uniform_u32(v);
   };
-  // metadata of slot k's entries (raw loads, all lanes the same address)
+  // Slot k's entries and their metadata -- scalar loads into SGPRs: the
+  // metadata of the next slot holds no vector registers across the chains
+  // (with vector loads the scheduler ran out of registers and serialised the
+  // two chains' LDS lookups)
   uint64_t mo0, mo1;
-  uint32_t mL0, mL1, mi0, mi1, mj0, mj1;
+  uint32_t mL0, mL1, ms0, ms1, mj0, mj1;
   auto meta = [&](uint32_t k) {
     const bool isb = k < nB;
     const uint32_t a = 2u * (k - nB);
-    mj0 = isb ? ((uint32_t)list[kHeadSub - 1u - k] | kTOk | kTPair) : (a < nA ? (uint32_t)list[a] | kTOk : 0u);
-    mj1 = isb ? mj0 : (a + 1u < nA ? (uint32_t)list[a + 1u] | kTOk : 0u);
-    const uint64_t i0 = sub0 + (mj0 & 1023u), i1 = sub0 + (mj1 & 1023u);
-    mo0 = g.offsets_at(i0);
-    mL0 = g.lengths_lo(i0);
-    mi0 = ibase[g.init ? i0 : 0u];
-    mo1 = g.offsets_at(i1);
-    mL1 = g.lengths_lo(i1);
-    mi1 = ibase[g.init ? i1 : 0u];
+    const uint32_t e0 = uniform_u32(isb ? (uint32_t)list[kHeadSub - 1u - k] : (a < nA ? (uint32_t)list[a] : 0u));
+    const uint32_t e1 = uniform_u32(isb || a + 1u >= nA ? 0u : (uint32_t)list[a + 1u]);
+    mj0 = isb ? (e0 | kTOk | kTPair) : (a < nA ? e0 | kTOk : 0u);
+    mj1 = isb ? mj0 : (a + 1u < nA ? e1 | kTOk : 0u);
+    g.meta_s(sub0 + (mj0 & 1023u), mo0, mL0, ms0);
+    g.meta_s(sub0 + (mj1 & 1023u), mo1, mL1, ms1);
   };
-  // positions of one entry (uniform: lane 0's copy); for a PAIR slot the
-  // first pass is the head, the second the body
-  auto pos = [&](uint64_t mo, uint32_t mL, uint32_t mi, uint32_t mj, bool second, SlotPass& q) {
-    const uint32_t tag = uniform_u32(mj);
-    const uint32_t L = uniform_u32(mL);  // (low word: see above)
-    const uint32_t h = ((L - 1u) & (kChunk - 1u)) + 1u;
-    const uintptr_t p = g.base_addr() + uniform_u64(mo);
-    const uint32_t s = ~(g.init ? uniform_u32(mi) : g.init_all);
+  // positions of one entry; for a PAIR slot the first pass is the head, the
+  // second the body
+  auto pos = [&](uint64_t o, uint32_t L, uint32_t s, uint32_t tag, bool second, SlotPass& q) {
+    const uint32_t h = ((L - 1u) & (kChunk - 1u)) + 1u;  // (L: the low word, see above)
+    const uintptr_t p = g.base_addr() + o;
     q.tag = tag;
     if (!(tag & kTOk)) {
       q.ce = safe + kChunk;
@@ -1639,19 +1646,17 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
     const uintptr_t a = (q.tag & kTInj) ? (uintptr_t)(ka.hc + sub0 + (q.tag & 1023u)) : safe;
     return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)a);
   };
-  uint32_t k = pull();
-  meta(k);
   SlotPass A, B;
-  pos(mo0, mL0, mi0, mj0, false, A);
-  pos(mo1, mL1, mi1, mj1, true, B);
-  k = pull();
-  meta(k);
+  meta(pull());
+  pos(mo0, mL0, ms0, mj0, false, A);
+  pos(mo1, mL1, ms1, mj1, true, B);
   Chunk cA, cB;
   load_general(A.ce, true, A.ps, lane, cA);
   load_general(B.ce, true, B.ps, lane, cB);
   uint32_t xA = aux_load(A), xB = aux_load(B);
   while (true) {
     if (!(A.tag & kTOk)) break;  // (a slot wholly past the end: its loads just drain)
+    meta(pull());  // the next slot's (lands while this slot's words are built)
     uint32_t w[2][16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[0][q] = cA.d[q];
@@ -1672,14 +1677,17 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
     // mixed batch whose body kernel re-runs this tile's two-chunk bodies
     const uint32_t hcA = iA ^ A.sx, hcB = iB ^ B.sx;
     const uint32_t uA = A.tag, uB = B.tag;
-    pos(mo0, mL0, mi0, mj0, false, A);
-    pos(mo1, mL1, mi1, mj1, true, B);
-    k = pull();
-    meta(k);
+    pos(mo0, mL0, ms0, mj0, false, A);
+    pos(mo1, mL1, ms1, mj1, true, B);
     load_general(A.ce, true, A.ps, lane, cA);
     load_general(B.ce, true, B.ps, lane, cB);
     xA = aux_load(A);
     xB = aux_load(B);
+    // (The scheduler sinks the second pass's loads into the chains below to
+    // keep the two chains' lookups interleaved; forcing every load ahead of
+    // the chains -- an asm memory barrier -- serialised the chains and
+    // measured 2-6 % slower on r and v; so did pinning the chain steps with
+    // sched_group_barrier.)
     uint32_t raws[2];
     chains<2, false>(lds, lb, w, lane, raws);
     // shift4096 spreads its lookups over the lanes of a quad: every lane runs it
@@ -1773,10 +1781,7 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     slice(w0, w1, gb, ge);
     const bool valid = gb + (uint64_t)lane < ge;
     const uint64_t i = gb + (uint64_t)lane;
-    const bool tiny = valid && lL < 4;
     const uint32_t J = valid ? chunks_for(lL) : 0u;
-    const uint64_t hl = lL - (uint64_t)kChunk * (J - 1u);
-    const bool pstart = ((lp >> 4) & 255u) == 0u;
       // the tile's plan (tile_scan's lpre / tiles) from the lanes' lengths:
       // the waves' slices are consecutive, so one wave scan + one barrier
       uint64_t x = J;
@@ -2304,8 +2309,9 @@ __device__ __forceinline__ void tiled_plan(uint8_t* lds, const VarGeom& g, const
   const uint32_t Gt = ka.tile_G;  // <= kMaxTiles (host)
   const uint64_t tot = t < Gt ? ka.tiles[2ull * t] : 0;
   const uint64_t mj = t < Gt ? ka.tiles[2ull * t + 1] : 0;
-  long_bufs = __syncthreads_or(mj > kBufsMaxJ ? 1 : 0) != 0;
   multi = __syncthreads_or(mj > 2 ? 1 : 0) != 0;
+  if (!multi) return;  // every tile finished by the head kernel (short mode): the caller returns too
+  long_bufs = __syncthreads_or(mj > kBufsMaxJ ? 1 : 0) != 0;
   uint64_t x = tot;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -2463,7 +2469,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes > kPermLdsBytes ? kFusedLdsBytes : kPermLdsBytes];
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1, B0, B1;
-  bool long_bufs, multi;
+  bool long_bufs = false, multi;
   tiled_plan<kGenWaves>(lds, gv, ka, C0, C1, long_bufs, B0, B1, multi);
   // Every tile's largest chunk count <= 2: the head kernel ran each tile in
   // short mode and finished every buffer (run_heads) -- nothing left here.

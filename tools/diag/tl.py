@@ -64,3 +64,15 @@ for k in (0, 3, 5, 7):
     if v.size:
         q = np.percentile(v, [0, 10, 50, 90, 100])
         print(f"abs t{k:<10d} " + " ".join(f"{x:8.2f}" for x in q))
+
+# per-workgroup end (16 waves each) by blockIdx % 8 (the XCD under round-robin placement)
+end = rel[:, 7]
+nw = len(end) // 16 * 16
+wg_end = np.nanmax(end[:nw].reshape(-1, 16), axis=1)
+wg_start = np.nanmin(rel[:nw, 0].reshape(-1, 16), axis=1)
+print("per-WG end p0/p10/p50/p90/p100:", " ".join(f"{x:.2f}" for x in np.percentile(wg_end, [0, 10, 50, 90, 100])))
+for x in range(8):
+    e = wg_end[x::8]
+    print(f"  b%8={x}: end p10 {np.percentile(e, 10):6.2f} p50 {np.median(e):6.2f} max {e.max():6.2f}  start p50 {np.median(wg_start[x::8]):5.2f}")
+order = np.argsort(wg_end)
+print("slowest WGs:", order[-8:].tolist(), "fastest:", order[:8].tolist())

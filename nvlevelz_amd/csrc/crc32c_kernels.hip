@@ -316,6 +316,9 @@ struct KArgs {
   // head kernel, no body kernel) -- for a fixed batch the host's decision,
   // for a tiled variable batch per tile, from its scan.
   uint32_t short_ok = 0;
+  // Chunk-parallel aligned batches (crc32c_chunks_kernel): the raw register
+  // of every 4 KiB chunk, folded per buffer by crc32c_fold_kernel.
+  uint32_t* raws = nullptr;
 };
 
 // floor(a / d) for wave-uniform a < 2^63, d > 0, from a double-precision
@@ -397,6 +400,35 @@ struct FixedGeom {
   __device__ __forceinline__ uint64_t unit_lo(uint64_t T, uint32_t u) const { return global_unit_lo<F>(T, u); }
   __device__ __forceinline__ void put_recs(const KArgs& ka, uint8_t*, uint32_t u, const Rec& h, const Rec& t) const {
     global_put_recs(ka, u, h, t);
+  }
+};
+
+// The J 4096-byte chunks of n aligned buffers (16-B aligned base and stride,
+// len = 4096 J) as n*J independent one-chunk "buffers" for scheduler A:
+// chunk t = buffer t / J, chunk t % J; only chunk 0 carries the buffer's
+// ~init.  Scheduler B walked a buffer's chunks through a serial
+// acc = shift4096(acc) ^ raw chain and ran ~10 % behind config 2's rate on
+// config 4 (5000 x 2 MiB); here every chunk is an independent pass whose raw
+// register goes to KArgs::raws, and crc32c_fold_kernel combines each
+// buffer's J raws (log-depth, ~0.1 % of the traffic).
+struct ChunkGeom {
+  static constexpr bool kTiled = false;
+  const uint8_t* base;
+  uint64_t stride, n;  // n: chunks (buffers * J)
+  uint32_t J, jsh;     // jsh = log2(J) when J is a power of two, else 64
+  const uint32_t* init;
+  uint32_t init_all;
+  __device__ __forceinline__ BufInfo info(uint64_t t) const {
+    uint64_t i, c;
+    if (jsh < 64u) {
+      i = t >> jsh;
+      c = t & (uint64_t)(J - 1u);
+    } else {
+      i = udiv_u(t, J);
+      c = t - i * J;
+    }
+    const uint32_t s = c == 0 ? ~(init ? ldc(init, i) : init_all) : 0u;
+    return BufInfo{base + i * stride + c * kChunk, kChunk, 1u, s};
   }
 };
 
@@ -843,8 +875,8 @@ __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane) {
 #endif
 constexpr uint32_t kTail = NVL_TAIL;
 
-template <int U, int NW = kWavesPerWG, int M = kAligned>
-__device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, uint8_t* lds) {
+template <int U, int NW = kWavesPerWG, int M = kAligned, class G = FixedGeom, bool kRaw = false>
+__device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
   const uint32_t wv = uniform_u32(threadIdx.x >> 6);
@@ -901,14 +933,20 @@ __device__ __forceinline__ void run_pairs(const FixedGeom& g, const KArgs& ka, u
       group_raw<M, U>(lds, lb, bis, cs, lane, cur, raws);
       if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < U; ++k) ka.out[gp[k].i] = finish(~raws[k], ka.flags);
+        for (int k = 0; k < U; ++k) {
+          if constexpr (kRaw) ka.raws[gp[k].i] = raws[k];
+          else ka.out[gp[k].i] = finish(~raws[k], ka.flags);
+        }
       }
     } else {  // the range's ragged last unit
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         if (ok[k]) {
           const uint32_t r = chunk_raw<M>(lds, lb, gp[k].bi, 0, lane, cur[k]);
-          if (lane == 0) ka.out[gp[k].i] = finish(~r, ka.flags);
+          if (lane == 0) {
+            if constexpr (kRaw) ka.raws[gp[k].i] = r;
+            else ka.out[gp[k].i] = finish(~r, ka.flags);
+          }
         }
       }
     }
@@ -2030,6 +2068,52 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
   else run_units<M, waves_of<M>()>(g, ka, lds);
 }
 
+// Aligned multi-chunk fixed batches (config 4): every 4 KiB chunk an
+// independent scheduler-A pass (ChunkGeom), raw registers to KArgs::raws.
+__global__ __launch_bounds__(kThreads, 1) void crc32c_chunks_kernel(ChunkGeom g, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  run_pairs<NVL_FAST_U, kWavesPerWG, kAligned, ChunkGeom, true>(g, ka, lds);
+}
+
+// Buffer i of J chunks: raw = XOR_c shift(raws[iJ + c], 4096 (J - 1 - c)).
+// One wave per buffer: lane l folds the R = ceil(J/64) raws of its run
+// [J - R(64 - l), J - R(63 - l)) serially through the shift-by-4096 operator
+// (byte-sliced, in LDS), shifts its run to the buffer end with one GF(2)
+// multiply by m_l = x^(8 * 4096 R (63 - l)) (built once per wave from the
+// x^(2^k) powers), and the 64 lanes XOR-reduce.
+__global__ __launch_bounds__(256) void crc32c_fold_kernel(const uint32_t* __restrict__ raws, uint64_t n, uint32_t J,
+                                                          const uint32_t* __restrict__ tables,
+                                                          uint32_t* __restrict__ out, uint32_t flags) {
+  __shared__ uint32_t sh[1024];  // sh4096[4][256]
+  for (uint32_t t = threadIdx.x; t < 1024u; t += blockDim.x) sh[t] = tables[kGComb + 6u * 1024u + t];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t R = (J + 63u) / 64u;
+  const uint32_t* x2n = tables + kGX2n;
+  uint32_t m = nvl::kOne, P = nvl::xpow8(x2n, (uint64_t)kChunk * R);
+  const uint32_t e = 63u - lane;
+  for (int b = 0; b < 6; ++b) {
+    if ((e >> b) & 1u) m = nvl::gf_mul(P, m);
+    P = nvl::gf_mul(P, P);
+  }
+  const uint64_t wpb = blockDim.x >> 6;
+  const uint64_t nw = (uint64_t)gridDim.x * wpb;
+  for (uint64_t i = (uint64_t)blockIdx.x * wpb + uniform_u32(threadIdx.x >> 6); i < n; i += nw) {
+    const int64_t c0 = (int64_t)J - (int64_t)R * (int64_t)(64u - lane);
+    const uint32_t* rb = raws + i * J;
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < R; ++k) {
+      const int64_t c = c0 + (int64_t)k;
+      const uint32_t r = c >= 0 ? rb[c] : 0u;
+      acc = sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)] ^ r;
+    }
+    acc = nvl::gf_mul(m, acc);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+    if (lane == 0) out[i] = finish(~acc, flags);
+  }
+}
+
 #ifndef NVL_VAR_BUFS
 #define NVL_VAR_BUFS 1  // 1: scheduler C when every buffer has <= kBufsMaxJ chunks
 #endif
@@ -2669,8 +2753,15 @@ static inline size_t recs_part(int num_cu, uint64_t len, uint64_t n) {
 }
 
 // Fixed-stride workspace: [unit records (J > 1)][hc: n u32 (partial first chunks with J > 1)]
+// or, for a shape that can take the chunk-parallel path (len a multiple of
+// 4096, J > 1: aligned when base and stride are), the n*J chunk raws if larger.
+static inline size_t chunk_raws_bytes(uint64_t len, uint64_t n) {
+  return (len > dev::kChunk && len % dev::kChunk == 0) ? n * (len / dev::kChunk) * sizeof(uint32_t) : 0;
+}
 size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
-  const size_t r = (recs_part(num_cu, len, n) + 255) / 256 * 256;
+  const size_t cr = chunk_raws_bytes(len, n);
+  const size_t r0 = (recs_part(num_cu, len, n) + 255) / 256 * 256;
+  const size_t r = r0 > cr ? r0 : cr;
   const bool hcs = n && chunks_of(len) > 1 && dev::head_first(len);
   return r + (hcs ? n * sizeof(uint32_t) : 0);
 }
@@ -2699,6 +2790,29 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
                                  body ? nullptr : lc.ev_stop);
     if (eh != hipSuccess || !body) return eh;
     ev_start = nullptr;
+  }
+  if (aligned && J > 1) {  // chunk-parallel: every chunk a scheduler-A pass, then the per-buffer fold
+    const uint64_t T = n * (uint64_t)J;
+    const uint32_t jsh = (J & (J - 1u)) == 0u ? (uint32_t)__builtin_ctz(J) : 64u;
+    dev::ChunkGeom cg{base, stride, T, J, jsh, init, init_all};
+    dev::KArgs kc{out, flags, nullptr, lc.tables, nullptr, nullptr};
+    kc.raws = reinterpret_cast<uint32_t*>(ws);
+    const uint32_t gc = grid_for(lc.num_cu, T);
+    if (ev_start)
+      hipExtLaunchKernelGGL(dev::crc32c_chunks_kernel, dim3(gc), dim3(dev::kThreads), 0, lc.stream, ev_start, nullptr,
+                            0u, cg, kc);
+    else
+      hipLaunchKernelGGL(dev::crc32c_chunks_kernel, dim3(gc), dim3(dev::kThreads), 0, lc.stream, cg, kc);
+    hipError_t ec = hipGetLastError();
+    if (ec != hipSuccess) return ec;
+    const uint32_t gf = (uint32_t)std::min<uint64_t>((n + 3) / 4, 65535);
+    if (lc.ev_stop)
+      hipExtLaunchKernelGGL(dev::crc32c_fold_kernel, dim3(gf), dim3(256), 0, lc.stream, nullptr, lc.ev_stop, 0u,
+                            kc.raws, n, J, lc.tables, out, flags);
+    else
+      hipLaunchKernelGGL(dev::crc32c_fold_kernel, dim3(gf), dim3(256), 0, lc.stream, kc.raws, n, J, lc.tables, out,
+                         flags);
+    return hipGetLastError();
   }
   dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc};
   hipEvent_t stop_main = J == 1 ? lc.ev_stop : nullptr;  // else the fix-up records it

@@ -408,3 +408,23 @@ def test_concurrent_threads_and_streams(dev, C, port):
     for t in th:
         t.join()
     assert not errs
+
+
+@pytest.mark.parametrize("J,n,gap", [(2, 300, 0), (3, 100, 4096), (64, 9, 16), (65, 5, 0), (512, 7, 0),
+                                     (1000, 3, 32), (127, 2, 4096 * 3)])
+def test_fixed_chunk_parallel(dev, C, port, J, n, gap):
+    """Aligned multi-chunk buffers (crc32c_chunks_kernel + crc32c_fold_kernel):
+    J below, at and above one lane run per lane (R = ceil(J/64)), powers of
+    two and not, gaps between buffers, per-buffer inits and Mask."""
+    L = 4096 * J
+    stride = L + gap
+    host = port.fill(0xC4 + J, 0, (n - 1) * stride + L)
+    buf = torch.from_numpy(host).to(dev)
+    rng = np.random.default_rng(J)
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    got = _u32(C.extend_fixed(buf, stride, L, n, torch.from_numpy(inits.view(np.int32)).to(dev)))
+    want = port.fixed(host, stride, L, n, inits)
+    assert np.array_equal(got, want)
+    got = _u32(C.extend_fixed(buf, stride, L, n, 0x0BADF00D, mask=True))
+    want = port.fixed(host, stride, L, n, np.full(n, 0x0BADF00D, dtype=np.uint32))
+    assert np.array_equal(got, np.array([port.mask(int(x)) for x in want], dtype=np.uint32))

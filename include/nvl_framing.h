@@ -90,6 +90,12 @@ NVL_API int nvl_sstable_verify_blocks(const void* file, uint64_t file_len, const
 
 #define NVL_BLOCK_BAD_HANDLE 4 /* the index/metaindex value is not a BlockHandle: "bad block handle"
                                   (Table::BlockReader table/table.cc:160-165); offset = size = 0 */
+#define NVL_BLOCK_UNCHECKED 5  /* NVL_TABLE_LIST_ONLY: listed, not yet checked */
+
+#define NVL_TABLE_LIST_ONLY 0x200u /* nvl_sstable_verify_table flag: list the blocks (footer, index and
+                                      metaindex read and checked on the host) without checking the meta
+                                      and data blocks -- Table::Open without the reads of the blocks an
+                                      iterator will touch; they get NVL_BLOCK_UNCHECKED */
 
 typedef struct nvl_table_block {
   uint64_t offset;
@@ -113,6 +119,10 @@ typedef struct nvl_table_block {
  * metaindex blocks are read and checked (host CRC, no batch); *n_blocks and
  * *table_status are then exact and *n_bad is left 0.  Compressed (type 1)
  * data/meta blocks verify as OK here, as in nvl_sstable_verify_blocks. */
+/* With NVL_TABLE_LIST_ONLY in flags the meta and data blocks are listed
+ * with NVL_BLOCK_UNCHECKED (no batch): the open of a batched table reader
+ * (nvl::shims::TableReader) that checks them per readahead window with
+ * nvl_sstable_verify_blocks.  *n_bad counts the blocks whose check failed. */
 NVL_API int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_block* blocks, size_t cap,
                                      size_t* n_blocks, uint32_t* table_status, uint64_t* n_bad, uint32_t flags);
 

@@ -9,6 +9,9 @@
 //   nvl::shims::LogWriter   db/log_writer.h:18-47, db/log_writer.cc:17-109
 //   nvl::shims::TableFile   TableBuilder::WriteRawBlock table/table_builder.cc:175-193
 //                           + the checks of ReadBlock table/format.cc:65-98
+//   nvl::shims::BatchingWritableFile  the WritableFile adapter around a table's file
+//   nvl::shims::TableReader Table::Open + Table::BlockReader table/table.cc:38-82,163-215,
+//                           checks batched per readahead window
 #ifndef NVL_LEVELDB_SHIMS_H_
 #define NVL_LEVELDB_SHIMS_H_
 
@@ -451,6 +454,196 @@ class TableFile {
  private:
   std::string image_;
   std::vector<nvl_block_handle> blocks_;
+};
+
+// ---------------------------------------------------------------------------
+// The writer-side adapter a LevelDB tree drops in around a table's file
+// (SURVEY.md §8f rank 1): TableBuilder writes into it through the ordinary
+// leveldb::WritableFile interface; WriteRawBlock's two Appends per block --
+// the contents, then the 5-byte trailer (table/table_builder.cc:175-193) --
+// stage the block with a placeholder CRC, and every staged trailer is sealed
+// (Mask(Value(block | type)), one GPU batch) when the staged bytes pass
+// `seal_bytes`, at Sync() and at Close(), before the bytes reach `target`.
+// Block offsets never depend on CRC values (fixed 5-byte trailer), so the
+// file is byte-identical to the reference builder's.  Flush() is a hint
+// TableBuilder gives after every data block (table_builder.cc:146): it seals
+// nothing, so a table's blocks batch together.  The template takes the
+// tree's own types: BatchingWritableFile<leveldb::WritableFile,
+// leveldb::Slice, leveldb::Status>.
+//
+// With the stock WriteRawBlock the reference still computes a CRC per block
+// and this adapter discards it; the two-line edit of INTEGRATION.md §5
+// (skip the CRC when DefersBlockCrc(r->file)) leaves the CRCs to the batch
+// alone.  DeferredBlockCrc is the marker that edit tests for.
+class DeferredBlockCrc {
+ public:
+  virtual ~DeferredBlockCrc() {}
+};
+
+// True when `file` (a leveldb::WritableFile*) seals block trailers itself.
+template <class F>
+inline bool DefersBlockCrc(F* file) {
+  return file != nullptr && dynamic_cast<DeferredBlockCrc*>(file) != nullptr;
+}
+
+template <class WritableFileT, class SliceT, class StatusT>
+class BatchingWritableFile : public WritableFileT, public DeferredBlockCrc {
+ public:
+  // target: receives every sealed byte (not owned; Close() closes it).
+  // flags: NVL_FRAMING_HOST for the host CRC.
+  explicit BatchingWritableFile(WritableFileT* target, uint64_t seal_bytes = 64ull << 20, uint32_t flags = 0)
+      : target_(target), seal_bytes_(seal_bytes), flags_(flags) {}
+
+  StatusT Append(const SliceT& data) override {
+    if (have_ && data.size() == NVL_BLOCK_TRAILER_SIZE) {  // the trailer of the pending block
+      const char* t = data.data();
+      computed_ += (t[1] | t[2] | t[3] | t[4]) != 0;  // a CRC the writer computed (discarded here)
+      const nvl_block_handle h = tf_.AppendBlock(pending_.data(), pending_.size(), (uint8_t)t[0]);
+      handles_.push_back(nvl_block_handle{written_ + h.offset, h.size});
+      have_ = false;
+      pending_.clear();
+      return tf_.size() >= seal_bytes_ ? Drain() : StatusT::OK();
+    }
+    StageRaw();
+    pending_.assign(data.data(), data.size());
+    have_ = true;
+    return StatusT::OK();
+  }
+  StatusT Flush() override { return StatusT::OK(); }
+  StatusT Sync() override {
+    StageRaw();
+    StatusT s = Drain();
+    return s.ok() ? target_->Sync() : s;
+  }
+  StatusT Close() override {
+    StageRaw();
+    StatusT s = Drain();
+    return s.ok() ? target_->Close() : s;
+  }
+
+  size_t seals() const { return seals_; }                    // batches issued
+  const std::string& staged() const { return tf_.image(); }  // (tests: the bytes before sealing)
+  // every block staged so far, {offset in the file, size}, in write order
+  const std::vector<nvl_block_handle>& handles() const { return handles_; }
+  // trailers that arrived with a nonzero CRC: the writer computed one (the
+  // stock WriteRawBlock); 0 with INTEGRATION.md §5's edit
+  size_t computed_crcs() const { return computed_; }
+
+ private:
+  // a pending Append that no trailer followed (the footer): plain bytes
+  void StageRaw() {
+    if (have_) tf_.Append(pending_.data(), pending_.size());
+    have_ = false;
+    pending_.clear();
+  }
+  // seal the staged trailers (one batch) and hand the bytes to the target
+  StatusT Drain() {
+    if (tf_.size() == 0) return StatusT::OK();
+    if (!tf_.blocks().empty()) {
+      const int rc = tf_.Seal(flags_);
+      ++seals_;
+      if (rc != NVL_CRC32C_OK) return StatusT::IOError(SliceT("nvl_sstable_seal_trailers"), SliceT(nvl_crc32c_strerror(rc)));
+    }
+    StatusT s = target_->Append(SliceT(tf_.image().data(), tf_.image().size()));
+    written_ += tf_.size();
+    tf_ = TableFile();
+    return s;
+  }
+
+  WritableFileT* target_;
+  uint64_t seal_bytes_;
+  uint32_t flags_;
+  TableFile tf_;
+  std::string pending_;
+  bool have_ = false;
+  size_t seals_ = 0;
+  size_t computed_ = 0;
+  uint64_t written_ = 0;
+  std::vector<nvl_block_handle> handles_;
+};
+
+// ---------------------------------------------------------------------------
+// The reader-side shim of SURVEY.md §8f rank 2: Table::Open (footer, index
+// and metaindex, table/table.cc:38-82) and Table::BlockReader
+// (table.cc:163-215, ReadBlock with verify_checksums) over a table image in
+// memory (an mmap'd file, util/env_posix.cc:199-209), with the checks of the
+// blocks an iterator touches batched per readahead window: the first read of
+// data block i checks data blocks [i, i + window) -- those not yet checked --
+// in one batch, as a compaction input scan (db/version_set.cc:1308,1329)
+// walks them in index order.  Meta blocks (the filter) are checked at Open in
+// one batch.  Verdicts are ReadBlock's (NVL_BLOCK_*); a block whose index
+// value is not a handle reads as NVL_BLOCK_BAD_HANDLE, as BlockReader's
+// "bad block handle".
+class TableReader {
+ public:
+  TableReader(const char* file, uint64_t file_len, size_t window_blocks = 64, uint32_t flags = 0)
+      : file_(file), len_(file_len), window_(window_blocks ? window_blocks : 1), flags_(flags) {}
+
+  // *table_status = NVL_TABLE_*; the index/metaindex and meta blocks listed
+  // and checked.  Returns the engine status.
+  int Open(uint32_t* table_status) {
+    size_t n = 0;
+    uint64_t bad = 0;
+    int rc = nvl_sstable_verify_table(file_, len_, nullptr, 0, &n, table_status, &bad, flags_);
+    if (rc != NVL_CRC32C_OK) return rc;
+    blocks_.resize(n);
+    rc = nvl_sstable_verify_table(file_, len_, blocks_.data(), n, &n, table_status, &bad,
+                                  flags_ | NVL_TABLE_LIST_ONLY);
+    if (rc != NVL_CRC32C_OK) return rc;
+    blocks_.resize(n);
+    data_.clear();
+    std::vector<size_t> meta;
+    for (size_t i = 0; i < blocks_.size(); ++i) {
+      if (blocks_[i].role == NVL_TBLOCK_DATA) data_.push_back(i);
+      if (blocks_[i].role == NVL_TBLOCK_META) meta.push_back(i);
+    }
+    return Check(meta);
+  }
+
+  size_t num_data_blocks() const { return data_.size(); }
+
+  // Data block i (index order): its handle and ReadBlock verdict; the block's
+  // contents are file + h->offset, h->size bytes.
+  int ReadDataBlock(size_t i, nvl_block_handle* h, uint32_t* verdict) {
+    if (i >= data_.size()) return NVL_CRC32C_EINVAL;
+    nvl_table_block& b = blocks_[data_[i]];
+    if (b.verdict == NVL_BLOCK_UNCHECKED) {
+      std::vector<size_t> win;
+      for (size_t k = i; k < data_.size() && win.size() < window_; ++k)
+        if (blocks_[data_[k]].verdict == NVL_BLOCK_UNCHECKED) win.push_back(data_[k]);
+      const int rc = Check(win);
+      if (rc != NVL_CRC32C_OK) return rc;
+    }
+    h->offset = b.offset;
+    h->size = b.size;
+    *verdict = b.verdict;
+    return NVL_CRC32C_OK;
+  }
+
+  // every listed block (index, metaindex, meta, data), with the verdicts so far
+  const std::vector<nvl_table_block>& blocks() const { return blocks_; }
+  size_t batches() const { return batches_; }
+
+ private:
+  int Check(const std::vector<size_t>& which) {
+    if (which.empty()) return NVL_CRC32C_OK;
+    std::vector<nvl_block_handle> h(which.size());
+    for (size_t k = 0; k < which.size(); ++k) h[k] = nvl_block_handle{blocks_[which[k]].offset, blocks_[which[k]].size};
+    std::vector<uint8_t> v(which.size(), NVL_BLOCK_OK);
+    const int rc = nvl_sstable_verify_blocks(file_, len_, h.data(), h.size(), v.data(), nullptr, flags_);
+    ++batches_;
+    if (rc != NVL_CRC32C_OK) return rc;
+    for (size_t k = 0; k < which.size(); ++k) blocks_[which[k]].verdict = v[k];
+    return NVL_CRC32C_OK;
+  }
+
+  const char* file_;
+  uint64_t len_;
+  size_t window_;
+  uint32_t flags_;
+  std::vector<nvl_table_block> blocks_;
+  std::vector<size_t> data_;
+  size_t batches_ = 0;
 };
 
 // ReadBlock's checks (format.cc:77-135) for every block of a table image in

@@ -340,7 +340,7 @@ uint8_t host_block_verdict(const std::vector<uint8_t>& b, uint64_t size) {
 // blocks are small: read to the host and checked there; every other block's
 // check goes to the source's batch.
 int verify_table_core(TableSource& src, uint64_t file_len, nvl_table_block* blocks, size_t cap, size_t* n_blocks,
-                      uint32_t* table_status, uint64_t* n_bad) {
+                      uint32_t* table_status, uint64_t* n_bad, bool list_only) {
   *table_status = NVL_TABLE_OK;
   if (file_len < NVL_FOOTER_SIZE) {  // table.cc:44-46
     *table_status = NVL_TABLE_TOO_SHORT;
@@ -405,7 +405,8 @@ int verify_table_core(TableSource& src, uint64_t file_len, nvl_table_block* bloc
     for (size_t i = 0; i < meta_blocks.size(); ++i) all.push_back(meta_blocks[i]);
     for (size_t i = 0; i < data_h.size(); ++i) all.push_back(data_h[i]);
     std::vector<uint8_t> verdict;
-    if ((rc = src.verify(all, &verdict)) != NVL_CRC32C_OK) return rc;
+    if (list_only) verdict.assign(all.size(), (uint8_t)NVL_BLOCK_UNCHECKED);
+    else if ((rc = src.verify(all, &verdict)) != NVL_CRC32C_OK) return rc;
     emit(index_h, NVL_TBLOCK_INDEX, v_index);
     emit(meta_h, NVL_TBLOCK_METAINDEX, v_meta);
     size_t k = 0;
@@ -418,7 +419,7 @@ int verify_table_core(TableSource& src, uint64_t file_len, nvl_table_block* bloc
   *n_blocks = out.size();
   if (n_bad) {
     uint64_t b = 0;
-    for (const nvl_table_block& t : out) b += t.verdict != NVL_BLOCK_OK;
+    for (const nvl_table_block& t : out) b += t.verdict != NVL_BLOCK_OK && t.verdict != NVL_BLOCK_UNCHECKED;
     *n_bad = b;
   }
   if (!blocks) return NVL_CRC32C_OK;
@@ -440,7 +441,8 @@ int nvl_sstable_verify_table(const void* file, uint64_t file_len, nvl_table_bloc
   src.f = static_cast<const uint8_t*>(file);
   src.len = file_len;
   src.flags = flags;
-  return nvl::verify_table_core(src, file_len, blocks, cap, n_blocks, table_status, n_bad);
+  return nvl::verify_table_core(src, file_len, blocks, cap, n_blocks, table_status, n_bad,
+                                (flags & NVL_TABLE_LIST_ONLY) != 0);
 }
 
 

@@ -30,8 +30,9 @@ inline bool block_in_file(const nvl_block_handle& h, uint64_t file_len) {
          file_len - h.size - h.offset >= (uint64_t)NVL_BLOCK_TRAILER_SIZE;
 }
 
+// list_only: NVL_TABLE_LIST_ONLY (meta and data blocks listed unchecked, no batch)
 int verify_table_core(TableSource& src, uint64_t file_len, nvl_table_block* blocks, size_t cap, size_t* n_blocks,
-                      uint32_t* table_status, uint64_t* n_bad);
+                      uint32_t* table_status, uint64_t* n_bad, bool list_only = false);
 
 }  // namespace nvl
 

@@ -326,18 +326,23 @@ class _RefTable:
     """ctypes view of ``oracle/_ref/libref_table.so`` (oracle/ref_table.cc): the
     reference's own TableBuilder, writing to memory or through shims::TableFile."""
 
-    def __init__(self) -> None:
-        self.path = os.path.join(HERE, "_ref", "libref_table.so")
+    def __init__(self, deferred: bool = False) -> None:
+        self.path = os.path.join(HERE, "_ref", "libref_table_deferred.so" if deferred else "libref_table.so")
         lib = ctypes.CDLL(self.path, mode=os.RTLD_LOCAL)
         vp, sz, u64, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32
         lib.ref_table_build.restype = ctypes.c_int
         lib.ref_table_build.argtypes = [vp, vp, vp, sz, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, vp, sz,
-                                        vp, vp, sz, vp]
+                                        vp, vp, sz, vp, vp, vp]
         self.lib = lib
 
-    def build(self, keys, values, block_size=4096, restart_interval=16, bloom_bits=0, via_shim=False,
+    def build(self, keys, values, block_size=4096, restart_interval=16, bloom_bits=0, via_shim=0,
               seal_flags=0):
-        """(image bytes, block handles [(offset, size)] -- via_shim only)."""
+        """(image bytes, block handles [(offset, size)] in write order -- via_shim
+        only).  via_shim: 0 the reference's own file; 1 / 2 the shipped
+        BatchingWritableFile sealing at Close / every ~5000 bytes; 3 its staged
+        bytes before any seal (oracle/ref_table.cc).  self.seals: the seal
+        batches of the last build; self.computed: the trailers that reached the
+        adapter with a CRC the builder computed itself."""
         kv = b"".join(k + v for k, v in zip(keys, values)) or b"\0"
         kl = np.array([len(k) for k in keys] or [0], dtype=np.uint64)
         vl = np.array([len(v) for v in values] or [0], dtype=np.uint64)
@@ -347,26 +352,30 @@ class _RefTable:
         hcap = 2 * (len(kv) // 16 + 64)
         hd = np.zeros(hcap, dtype=np.uint64)
         nh = ctypes.c_size_t(0)
+        seals = ctypes.c_size_t(0)
+        computed = ctypes.c_size_t(0)
         rc = self.lib.ref_table_build(kv, kl.ctypes.data, vl.ctypes.data, len(keys), block_size, restart_interval,
                                       bloom_bits, int(via_shim), seal_flags, out, cap, ctypes.byref(n),
-                                      hd.ctypes.data, hcap, ctypes.byref(nh))
+                                      hd.ctypes.data, hcap, ctypes.byref(nh), ctypes.byref(seals),
+                                      ctypes.byref(computed))
         assert rc == 0, rc
+        self.seals = seals.value
+        self.computed = computed.value
         hs = [(int(hd[2 * k]), int(hd[2 * k + 1])) for k in range(nh.value)]
         return out.raw[:n.value], hs
 
 
-_ref_table = None
+_ref_table = {}
 
 
-def ref_table():
-    global _ref_table
-    if _ref_table is None:
-        _ref_table = _RefTable()
-    return _ref_table
+def ref_table(deferred: bool = False):
+    if deferred not in _ref_table:
+        _ref_table[deferred] = _RefTable(deferred)
+    return _ref_table[deferred]
 
 
-def ref_table_available() -> bool:
-    return os.path.exists(os.path.join(HERE, "_ref", "libref_table.so"))
+def ref_table_available(deferred: bool = False) -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libref_table_deferred.so" if deferred else "libref_table.so"))
 
 
 def ref_framing_available() -> bool:

@@ -12,12 +12,21 @@
 // found; at -O0 the function returns normally.  No stand-in Env is used.
 //
 // ref_table_build drives one key/value sequence through TableBuilder into
-//   via_shim = 0: an in-memory WritableFile (the reference's file), or
-//   via_shim = 1: a WritableFile that routes every block through
-//                 nvl::shims::TableFile -- contents appended, the 5-byte
-//                 trailer replaced by the block type with a zero CRC -- and
-//                 seals all trailers in one engine batch (nvl_sstable_seal_trailers).
-// The two images must be byte-identical.  Nothing here is product code.
+//   via_shim = 0: an in-memory WritableFile (the reference's file), or the
+//   shipped adapter nvl::shims::BatchingWritableFile<leveldb::WritableFile,
+//   leveldb::Slice, leveldb::Status> (include/nvl_leveldb_shims.h) around it:
+//   via_shim = 1: trailers sealed in one engine batch at Close();
+//   via_shim = 2: sealed every ~5000 staged bytes (many batches);
+//   via_shim = 3: the adapter's staged bytes before any seal.
+// *computed: the trailers that reached the adapter with a CRC TableBuilder
+// computed itself (every block with the stock WriteRawBlock, none with the
+// edit).
+// Built twice by oracle/Makefile: libref_table.so with the reference's
+// table_builder.cc as it is (WriteRawBlock computes a CRC the adapter
+// discards) and libref_table_deferred.so with INTEGRATION.md §5's edit
+// applied at build time by apply_deferred_crc.py (WriteRawBlock leaves the
+// CRC to the file when nvl::shims::DefersBlockCrc(file)).  The images of
+// modes 0-2 must be byte-identical.  Nothing here is product code.
 #include <stdint.h>
 #include <string.h>
 
@@ -45,34 +54,7 @@ class StringSink : public leveldb::WritableFile {
   leveldb::Status Sync() override { return leveldb::Status::OK(); }
 };
 
-// TableBuilder::WriteRawBlock appends a block's contents, then its 5-byte
-// trailer (table_builder.cc:175-193); Finish appends the 48-byte footer.
-class SealSink : public leveldb::WritableFile {
- public:
-  nvl::shims::TableFile tf;
-  leveldb::Status Append(const leveldb::Slice& d) override {
-    if (have_ && d.size() == NVL_BLOCK_TRAILER_SIZE) {  // the trailer of the pending block
-      tf.AppendBlock(pending_.data(), pending_.size(), (uint8_t)d[0]);
-      have_ = false;
-      return leveldb::Status::OK();
-    }
-    Flush1();
-    pending_.assign(d.data(), d.size());
-    have_ = true;
-    return leveldb::Status::OK();
-  }
-  void Flush1() {
-    if (have_) tf.Append(pending_.data(), pending_.size());
-    have_ = false;
-  }
-  leveldb::Status Close() override { return leveldb::Status::OK(); }
-  leveldb::Status Flush() override { return leveldb::Status::OK(); }
-  leveldb::Status Sync() override { return leveldb::Status::OK(); }
-
- private:
-  std::string pending_;
-  bool have_ = false;
-};
+typedef nvl::shims::BatchingWritableFile<leveldb::WritableFile, leveldb::Slice, leveldb::Status> BatchingFile;
 
 }  // namespace
 
@@ -82,7 +64,8 @@ extern "C" {
 __attribute__((visibility("default")))
 int ref_table_build(const uint8_t* kv, const uint64_t* klen, const uint64_t* vlen, size_t n, uint64_t block_size,
                     int restart_interval, int bloom_bits, int via_shim, uint32_t seal_flags, uint8_t* out, size_t cap,
-                    size_t* out_len, uint64_t* handles, size_t hcap, size_t* nh) {
+                    size_t* out_len, uint64_t* handles, size_t hcap, size_t* nh, size_t* seals,
+                    size_t* computed) {
   leveldb::Options opt;
   opt.block_size = (size_t)block_size;
   opt.block_restart_interval = restart_interval;
@@ -90,25 +73,27 @@ int ref_table_build(const uint8_t* kv, const uint64_t* klen, const uint64_t* vle
   const leveldb::FilterPolicy* fp = bloom_bits > 0 ? leveldb::NewBloomFilterPolicy(bloom_bits) : nullptr;
   opt.filter_policy = fp;
   StringSink plain;
-  SealSink seal;
-  leveldb::WritableFile* f = via_shim ? static_cast<leveldb::WritableFile*>(&seal) : &plain;
+  BatchingFile batch(&plain, via_shim == 2 ? 5000u : (via_shim == 3 ? ~0ull : 64ull << 20), seal_flags);
+  leveldb::WritableFile* f = via_shim ? static_cast<leveldb::WritableFile*>(&batch) : &plain;
   leveldb::TableBuilder tb(opt, f);
   const char* p = reinterpret_cast<const char*>(kv);
   for (size_t i = 0; i < n; ++i) {
     tb.Add(leveldb::Slice(p, klen[i]), leveldb::Slice(p + klen[i], vlen[i]));
     p += klen[i] + vlen[i];
   }
-  const leveldb::Status s = tb.Finish();
+  leveldb::Status s = tb.Finish();
   delete fp;
   if (!s.ok()) return 100;
-  const std::string* img = &plain.data;
+  std::string staged;
+  if (via_shim == 3) staged = batch.staged();  // (the footer is still pending: Finish's last Append)
+  if (via_shim) s = f->Close();
+  if (!s.ok()) return 101;
+  const std::string* img = via_shim == 3 ? &staged : &plain.data;
+  *seals = via_shim ? batch.seals() : 0;
+  *computed = via_shim ? batch.computed_crcs() : 0;
   *nh = 0;
   if (via_shim) {
-    seal.Flush1();
-    const int rc = seal.tf.Seal(seal_flags);
-    if (rc != NVL_CRC32C_OK) return rc;
-    img = &seal.tf.image();
-    const std::vector<nvl_block_handle>& b = seal.tf.blocks();
+    const std::vector<nvl_block_handle>& b = batch.handles();
     *nh = b.size();
     for (size_t k = 0; k < b.size() && 2 * k + 1 < hcap; ++k) {
       handles[2 * k] = b[k].offset;

@@ -163,4 +163,36 @@ int shim_table_verify(const uint8_t* file, size_t len, uint32_t flags, char* tra
   return copy_out(t, trace, cap, trace_len);
 }
 
+// nvl::shims::TableReader: Open, then every data block read in index order
+// (order 0) or backwards (order 1) with `window` blocks checked per batch;
+// the trace has shim_table_verify's format (every listed block with its
+// verdict after the reads) and *batches the verify batches issued.
+int shim_table_read(const uint8_t* file, size_t len, size_t window, uint32_t flags, int order, char* trace, size_t cap,
+                    size_t* trace_len, size_t* batches) {
+  nvl::shims::TableReader tr(reinterpret_cast<const char*>(file), len, window, flags);
+  uint32_t status = 0;
+  int rc = tr.Open(&status);
+  if (rc != NVL_CRC32C_OK) return rc;
+  const size_t nd = tr.num_data_blocks();
+  for (size_t k = 0; k < nd; ++k) {
+    const size_t i = order ? nd - 1 - k : k;
+    nvl_block_handle h;
+    uint32_t v = 0;
+    if ((rc = tr.ReadDataBlock(i, &h, &v)) != NVL_CRC32C_OK) return rc;
+  }
+  const std::vector<nvl_table_block>& blocks = tr.blocks();
+  uint64_t n_bad = 0;
+  for (size_t i = 0; i < blocks.size(); ++i) n_bad += blocks[i].verdict != NVL_BLOCK_OK;
+  char buf[96];
+  snprintf(buf, sizeof(buf), "%u %llu\n", status, (unsigned long long)n_bad);
+  std::string t(buf);
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    snprintf(buf, sizeof(buf), "%llu %llu %u %u\n", (unsigned long long)blocks[i].offset,
+             (unsigned long long)blocks[i].size, blocks[i].role, blocks[i].verdict);
+    t.append(buf);
+  }
+  *batches = tr.batches();
+  return copy_out(t, trace, cap, trace_len);
+}
+
 }  // extern "C"

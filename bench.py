@@ -148,20 +148,12 @@ def _varint(v: int) -> bytes:
     return bytes(out)
 
 
-def shim_bench(nblocks: int = 100_000) -> dict:
-    """nvl_sstable_verify_table (include/nvl_framing.h) over a host-resident
-    SSTable image of `nblocks` 4 KiB data blocks (table/format.h layout: one
-    key-value entry + restart array per block, 5-byte trailers, an index with
-    one BlockHandle per block, an empty metaindex, the 48-byte footer), as a
-    caller with an mmap'd table would run it: file bytes in host memory ->
-    one staging copy + H2D + batch kernel + D2H of the CRCs.  Beside it, the
-    same walk with the host CRC (NVL_FRAMING_HOST) and, where the reference
-    build exists, the reference's own Footer/ReadBlock/Block::Iter scan
-    (oracle/_ref, single thread) -- the CPU legs are reported baselines."""
+def build_table_image(nblocks: int, S: int = 4096) -> bytes:
+    """The shim bench's SSTable image (see shim_bench): nblocks data blocks of
+    S bytes, an empty metaindex, a restart-interval-1 index, the footer."""
     import ctypes
     from nvlevelz_amd import _lib
     L = _lib.lib
-    S = 4096
     key_len = 16
     hdr = _varint(0) + _varint(key_len)
     vlen = S - 8 - key_len - len(hdr) - 2
@@ -204,8 +196,23 @@ def shim_bench(nblocks: int = 100_000) -> dict:
     index_h = raw_block(index)
     foot = _varint(meta_h[0]) + _varint(meta_h[1]) + _varint(index_h[0]) + _varint(index_h[1])
     data.extend(foot + bytes(40 - len(foot)) + (0xDB4775248B80FB57).to_bytes(8, "little"))
-    image = bytes(data)
-    del data
+    return bytes(data)
+
+
+def shim_bench(nblocks: int = 100_000) -> dict:
+    """nvl_sstable_verify_table (include/nvl_framing.h) over a host-resident
+    SSTable image of `nblocks` 4 KiB data blocks (table/format.h layout: one
+    key-value entry + restart array per block, 5-byte trailers, an index with
+    one BlockHandle per block, an empty metaindex, the 48-byte footer), as a
+    caller with an mmap'd table would run it: file bytes in host memory ->
+    one staging copy + H2D + batch kernel + D2H of the CRCs.  Beside it, the
+    same walk with the host CRC (NVL_FRAMING_HOST) and, where the reference
+    build exists, the reference's own Footer/ReadBlock/Block::Iter scan
+    (oracle/_ref, single thread) -- the CPU legs are reported baselines."""
+    import ctypes
+    from nvlevelz_amd import _lib
+    L = _lib.lib
+    image = build_table_image(nblocks)
     nbytes = len(image)
 
     cap = nblocks + 2
@@ -245,13 +252,13 @@ def shim_bench(nblocks: int = 100_000) -> dict:
     del dimg
     res = {"what": "nvl_sstable_verify_table on a host-resident table image (footer -> index -> every block), "
                    "wall clock per call, median",
-           "table": {"data_blocks": nblocks, "block_bytes": S, "file_bytes": nbytes},
+           "table": {"data_blocks": nblocks, "block_bytes": 4096, "file_bytes": nbytes},
            "gpu": {"ms": round(t_gpu * 1e3, 3), "GiB/s": round(nbytes / t_gpu / 2**30, 3),
                    "path": "host image -> pinned staging -> H2D -> one batch kernel -> D2H"},
            "gpu_device_resident": {"ms": round(t_dev * 1e3, 3), "GiB/s": round(nbytes / t_dev / 2**30, 3),
-                                   "path": "image in HBM: footer/index/metaindex D2H + host parse, one batch "
-                                           "kernel + trailer-check kernel in place, verdicts D2H "
-                                           "(nvl_sstable_verify_table_dev)"},
+                                   "path": "image in HBM: footer + metaindex D2H, index block parsed on "
+                                           "the GPU, one batch over every block + trailer-check kernel in "
+                                           "place, records D2H (nvl_sstable_verify_table_dev)"},
            "host_crc": {"ms": round(t_host * 1e3, 3), "GiB/s": round(nbytes / t_host / 2**30, 3), "cores": 1,
                         "path": "same walk, NVL_FRAMING_HOST"}}
     try:

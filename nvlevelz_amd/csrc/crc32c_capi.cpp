@@ -392,6 +392,37 @@ struct HostPipe {
   }
 };
 
+// A per-thread device buffer (nvl_sstable_verify_table_dev's workspace),
+// grown on demand; rebuilt when the device or the engine generation changes.
+struct DevSlab {
+  int device = -1;
+  uint64_t gen = 0;
+  void* p = nullptr;
+  size_t cap = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    device = -1;
+  }
+  void* get(int dev, size_t bytes) {
+    const uint64_t g = g_generation.load(std::memory_order_acquire);
+    if (dev == device && g == gen && bytes <= cap && p) return p;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (device >= 0 && device != prev) (void)hipSetDevice(device);
+    release();
+    (void)hipSetDevice(dev);
+    if (hipMalloc(&p, bytes) != hipSuccess) p = nullptr;
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    if (!p) return nullptr;
+    device = dev;
+    gen = g;
+    cap = bytes;
+    return p;
+  }
+};
+
 // Everything a thread acquires for the host-resident entry points: one
 // non-blocking stream per device (a stream per call would also mean a
 // counter block per call), the pinned staging buffer and the fixed_host
@@ -407,6 +438,9 @@ struct ThreadRes {
   hipStream_t st[kMaxDevices] = {};
   Staging staging;
   HostPipe pipe;
+  DevSlab table_dev;      // nvl_sstable_verify_table_dev
+  Staging table_pinned;
+  hipEvent_t table_ev[kMaxDevices][2] = {};
   bool registered = false;
 
   void enroll() {
@@ -420,6 +454,12 @@ struct ThreadRes {
     int prev = -1;
     (void)hipGetDevice(&prev);
     for (int d = 0; d < kMaxDevices; ++d) {
+      for (hipEvent_t& e : table_ev[d]) {
+        if (!e) continue;
+        (void)hipSetDevice(d);
+        (void)hipEventDestroy(e);
+        e = nullptr;
+      }
       if (!st[d]) continue;
       (void)hipSetDevice(d);
       (void)hipStreamSynchronize(st[d]);
@@ -429,7 +469,10 @@ struct ThreadRes {
     }
     if (pipe.device >= 0) (void)hipSetDevice(pipe.device);
     pipe.release();
+    if (table_dev.device >= 0) (void)hipSetDevice(table_dev.device);
+    table_dev.release();
     staging.release();
+    table_pinned.release();
     if (prev >= 0) (void)hipSetDevice(prev);
   }
   ~ThreadRes() {
@@ -455,6 +498,37 @@ struct ThreadRes {
 thread_local ThreadRes t_res;
 
 hipStream_t thread_stream(int device) { return t_res.stream(device); }
+
+}  // namespace
+
+void* thread_table_device(int device, size_t bytes) {
+  t_res.enroll();
+  return t_res.table_dev.get(device, bytes);
+}
+
+void* thread_table_pinned(size_t bytes) {
+  t_res.enroll();
+  return t_res.table_pinned.get(bytes);
+}
+
+bool thread_table_aux(int device, hipStream_t* side, hipEvent_t* ev_a, hipEvent_t* ev_b) {
+  if (device < 0 || device >= kMaxDevices) return false;
+  *side = t_res.stream(device);  // enrolls
+  hipEvent_t* e = t_res.table_ev[device];
+  if (!e[0] || !e[1]) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (prev != device) (void)hipSetDevice(device);
+    for (int k = 0; k < 2; ++k)
+      if (!e[k] && hipEventCreateWithFlags(&e[k], hipEventDisableTiming) != hipSuccess) e[k] = nullptr;
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+  }
+  *ev_a = e[0];
+  *ev_b = e[1];
+  return *side && e[0] && e[1];
+}
+
+namespace {
 
 }  // namespace
 }  // namespace nvl

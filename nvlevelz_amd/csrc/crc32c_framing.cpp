@@ -55,12 +55,12 @@ struct BlockParse {
   nvl_log_event closing;    // BAD_LENGTH / ZERO / EOF, or kind = UINT32_MAX (none: trailer skipped)
 };
 
-// ---- SSTable structure (whole-table verify) --------------------------------
+}  // namespace
 
-constexpr uint64_t kTableMagic = 0xdb4775248b80fb57ull;  // table/format.h:77
+// ---- SSTable structure (whole-table verify; crc32c_framing_core.h) ---------
 
 // GetVarint64Ptr / GetVarint32Ptr (util/coding.cc): at most 10 / 5 bytes, never past limit.
-const uint8_t* get_varint(const uint8_t* p, const uint8_t* limit, unsigned max_shift, uint64_t* v) {
+static const uint8_t* get_varint(const uint8_t* p, const uint8_t* limit, unsigned max_shift, uint64_t* v) {
   uint64_t r = 0;
   for (unsigned shift = 0; shift <= max_shift && p < limit; shift += 7) {
     const uint64_t b = *p++;
@@ -125,7 +125,6 @@ uint32_t block_handles(const uint8_t* data, uint64_t size, std::vector<nvl_block
   return NVL_TABLE_OK;
 }
 
-}  // namespace
 }  // namespace nvl
 
 using namespace nvl;
@@ -325,15 +324,14 @@ struct HostTable : TableSource {
   }
 };
 
-// ReadBlock's trailer checks on one block held on the host with its trailer.
-uint8_t host_block_verdict(const std::vector<uint8_t>& b, uint64_t size) {
-  const uint32_t crc = host_extend(0, b.data(), size + 1);
-  if (crc != unmask(load_le32(b.data() + size + 1))) return NVL_BLOCK_CHECKSUM_MISMATCH;
+}  // namespace
+
+uint8_t host_block_verdict(const uint8_t* b, uint64_t size) {
+  const uint32_t crc = host_extend(0, b, size + 1);
+  if (crc != unmask(load_le32(b + size + 1))) return NVL_BLOCK_CHECKSUM_MISMATCH;
   if (b[size] != 0 && b[size] != 1) return NVL_BLOCK_BAD_TYPE;
   return NVL_BLOCK_OK;
 }
-
-}  // namespace
 
 // Table::Open (table/table.cc:38-82), then ReadBlock with verify_checksums of
 // every block the index and metaindex point at.  The index and metaindex
@@ -367,12 +365,12 @@ int verify_table_core(TableSource& src, uint64_t file_len, nvl_table_block* bloc
   if (block_in_file(index_h, file_len)) {
     index_b.resize(index_h.size + NVL_BLOCK_TRAILER_SIZE);
     if ((rc = src.read(index_h.offset, index_b.size(), index_b.data())) != NVL_CRC32C_OK) return rc;
-    v_index = host_block_verdict(index_b, index_h.size);
+    v_index = host_block_verdict(index_b.data(), index_h.size);
   }
   if (block_in_file(meta_h, file_len)) {
     meta_b.resize(meta_h.size + NVL_BLOCK_TRAILER_SIZE);
     if ((rc = src.read(meta_h.offset, meta_b.size(), meta_b.data())) != NVL_CRC32C_OK) return rc;
-    v_meta = host_block_verdict(meta_b, meta_h.size);
+    v_meta = host_block_verdict(meta_b.data(), meta_h.size);
   }
   std::vector<nvl_block_handle> data_h, meta_blocks;
   std::vector<uint8_t> data_bad, meta_bad;

@@ -12,6 +12,7 @@
 
 #include "crc32c_framing_core.h"
 #include "crc32c_internal.h"
+#include "crc32c_math.h"
 #include "nvl_crc32c.h"
 #include "nvl_framing.h"
 
@@ -43,8 +44,10 @@ struct DeviceTable : TableSource {
     if (m == 0) return NVL_CRC32C_OK;
     const size_t wsb = nvl_crc32c_batch_workspace_bytes(m);
     const size_t a = (m * 8 + 255) / 256 * 256, c = (m * 4 + 255) / 256 * 256;
-    uint8_t* d = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&d), 2 * a + c + a + wsb, st) != hipSuccess) return NVL_CRC32C_EHIP;
+    int dev = 0;
+    if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) return NVL_CRC32C_EHIP;
+    uint8_t* d = static_cast<uint8_t*>(thread_table_device(dev, 2 * a + c + a + wsb));
+    if (!d) return NVL_CRC32C_EHIP;
     uint64_t* doff = reinterpret_cast<uint64_t*>(d);
     uint64_t* dlen = reinterpret_cast<uint64_t*>(d + a);
     uint32_t* dcrc = reinterpret_cast<uint32_t*>(d + 2 * a);
@@ -61,12 +64,202 @@ struct DeviceTable : TableSource {
                                   hipStreamSynchronize(st) != hipSuccess))
         rc = NVL_CRC32C_EHIP;
     }
-    (void)hipFreeAsync(d, st);
-    if (rc != NVL_CRC32C_OK) return rc;
+    if (rc != NVL_CRC32C_OK) {
+      (void)hipStreamSynchronize(st);  // the workspace is the thread's: nothing may still use it
+      return rc;
+    }
     for (size_t k = 0; k < m; ++k) (*verdict)[which[k]] = v[k];
     return NVL_CRC32C_OK;
   }
 };
+
+inline uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+inline size_t up256(size_t x) { return (x + 255) / 256 * 256; }
+
+constexpr uint64_t kTailWin = 4096;       // last bytes of the file read first: footer (+ index tail, usually)
+constexpr uint64_t kMetaMax = 64u << 10;  // metaindex (+ trailer) bytes the fast path reads
+constexpr uint64_t kIndexPiece = 4096;    // the index block is checked as pieces of this size (crc32c_table_dev.hip)
+constexpr uint64_t kResHead = 32;         // device results: u32 bad, pad, u64 n_bad, u64 n_fix, pad
+constexpr uint8_t kCompute = 0xFF;
+
+// CRC32C(A || B) = shift(CRC32C(A), |B|) ^ CRC32C(B): the index block's
+// Value from its pieces' Values, with "shift by kIndexPiece bytes" as a
+// byte-sliced operator table (crc32c_math.h).
+struct PieceFold {
+  PowTable pt;
+  uint32_t op[4][256];
+  PieceFold() {
+    build_pow_table(&pt);
+    build_shift_op(pt.x2n, kIndexPiece, op);
+  }
+  uint32_t fold(const uint32_t* crc, uint64_t np, uint64_t total) const {
+    uint32_t u = 0;
+    for (uint64_t k = 0; k + 1 < np; ++k)
+      u = (op[0][u & 255] ^ op[1][(u >> 8) & 255] ^ op[2][(u >> 16) & 255] ^ op[3][u >> 24]) ^ crc[k];
+    const uint64_t last = total - (np - 1) * kIndexPiece;
+    return shift_bytes(pt.x2n, u, last) ^ crc[np - 1];
+  }
+};
+
+// *done = false: the caller runs the generic core (nothing written here is
+// kept).  On *done = true the result is final.
+//
+// Streams: on `st` the metaindex copy, the index parse (data slots and
+// records), the batch over data blocks + index pieces + meta blocks, the
+// trailer checks and the results copy; on the thread's side stream, once the
+// parse is done, the records copy into the caller's array -- it overlaps the
+// batch.  Records carry the verdict OK for every checked block; only when a
+// check fails (n_fix > 0) are the verdicts copied and patched in.
+int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t cap, size_t* n_blocks,
+               uint32_t* table_status, uint64_t* n_bad, hipStream_t st, bool* done) {
+  *done = false;
+  if (!blocks || len < NVL_FOOTER_SIZE) return NVL_CRC32C_OK;
+  int dev = 0;
+  if (st ? hipStreamGetDevice(st, &dev) != hipSuccess : hipGetDevice(&dev) != hipSuccess) return NVL_CRC32C_EHIP;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_meta = nullptr, ev_parse = nullptr;
+  if (!thread_table_aux(dev, &side, &ev_meta, &ev_parse)) return NVL_CRC32C_EHIP;
+  uint8_t* pin = static_cast<uint8_t*>(thread_table_pinned(kTailWin));
+  if (!pin) return NVL_CRC32C_EHIP;
+  // 1. the file's last bytes: the footer, and the index block's tail when
+  //    the index ends there (TableBuilder writes it last, table_builder.cc:241-266)
+  const uint64_t w = len < kTailWin ? len : kTailWin, w0 = len - w;
+  if (hipMemcpyAsync(pin, f + w0, w, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return NVL_CRC32C_EHIP;
+  const uint8_t* footer = pin + w - NVL_FOOTER_SIZE;
+  const uint64_t magic = (uint64_t)le32(footer + 40) | ((uint64_t)le32(footer + 44) << 32);
+  nvl_block_handle meta_h, index_h;
+  const uint8_t* fp = decode_handle(footer, footer + NVL_FOOTER_SIZE, &meta_h);
+  if (magic != kTableMagic || !fp || !decode_handle(fp, footer + NVL_FOOTER_SIZE, &index_h) ||
+      !block_in_file(index_h, len) || index_h.size < 4)
+    return NVL_CRC32C_OK;
+  const bool meta_in = block_in_file(meta_h, len);
+  if (meta_in && meta_h.size + NVL_BLOCK_TRAILER_SIZE > kMetaMax) return NVL_CRC32C_OK;
+  // the index tail: num_restarts (its last 4 bytes), type byte, masked CRC
+  const uint64_t tail_off = index_h.offset + index_h.size - 4;
+  uint8_t tail[9];
+  if (tail_off >= w0) {
+    memcpy(tail, pin + (tail_off - w0), 9);
+  } else if (hipMemcpyAsync(pin, f + tail_off, 9, hipMemcpyDeviceToHost, st) != hipSuccess ||
+             hipStreamSynchronize(st) != hipSuccess) {
+    return NVL_CRC32C_EHIP;
+  } else {
+    memcpy(tail, pin, 9);
+  }
+  const uint64_t nr = le32(tail);
+  if (tail[4] != 0 || nr == 0 || nr > (index_h.size - 4) / 4 || nr > 0xFFFFFFFFull - (1u << 24))
+    return NVL_CRC32C_OK;  // compressed / bad type / empty or bad restart array: the generic walk
+  const uint64_t ilen = index_h.size + 1;
+  const uint64_t np = (ilen + kIndexPiece - 1) / kIndexPiece;
+  if (np > (1u << 24)) return NVL_CRC32C_OK;
+  const uint64_t nm_max = meta_in ? meta_h.size / 3 + 1 : 0;  // entries take >= 3 bytes
+  if (2 + nr > cap) return NVL_CRC32C_OK;                     // the generic walk reports ENOSPC
+
+  // 2. device workspace: [results][boff][blen][crc][vk][records][batch workspace]
+  const uint64_t nmax = nr + np + nm_max;
+  const size_t s_res = up256(kResHead + 4 * np + nm_max), s8 = up256(nmax * 8), s4 = up256(nmax * 4),
+               s1 = up256(nmax), s_rec = up256(nr * sizeof(nvl_table_block));
+  const size_t wsb = nvl_crc32c_batch_workspace_bytes(nmax);
+  uint8_t* d = static_cast<uint8_t*>(thread_table_device(dev, s_res + 2 * s8 + s4 + s1 + s_rec + wsb));
+  if (!d) return NVL_CRC32C_EHIP;
+  uint8_t* dres = d;
+  uint64_t* boff = reinterpret_cast<uint64_t*>(d + s_res);
+  uint64_t* blen = reinterpret_cast<uint64_t*>(d + s_res + s8);
+  uint32_t* crc = reinterpret_cast<uint32_t*>(d + s_res + 2 * s8);
+  uint8_t* vk = d + s_res + 2 * s8 + s4;
+  nvl_table_block* rec = reinterpret_cast<nvl_table_block*>(d + s_res + 2 * s8 + s4 + s1);
+  void* ws = d + s_res + 2 * s8 + s4 + s1 + s_rec;
+  // pinned: [metaindex][meta slots: off, len1 | vk][results]
+  const size_t p_meta = 0, p_slots = up256(kMetaMax), p_res = p_slots + up256(nm_max * 17);
+  pin = static_cast<uint8_t*>(thread_table_pinned(p_res + s_res));
+  if (!pin) return NVL_CRC32C_EHIP;
+
+  // 3. on st: the metaindex copy, then the index parse; the host waits for
+  //    the copy only
+  if (hipMemsetAsync(dres, 0, kResHead, st) != hipSuccess) return NVL_CRC32C_EHIP;
+  if (meta_in && hipMemcpyAsync(pin + p_meta, f + meta_h.offset, meta_h.size + NVL_BLOCK_TRAILER_SIZE,
+                                hipMemcpyDeviceToHost, st) != hipSuccess)
+    return NVL_CRC32C_EHIP;
+  if (hipEventRecord(ev_meta, st) != hipSuccess ||
+      launch_index_entries(f, len, index_h.offset, index_h.size, (uint32_t)nr, (uint32_t)np, boff, blen, vk, rec,
+                           reinterpret_cast<uint32_t*>(dres), st) != hipSuccess ||
+      hipEventRecord(ev_parse, st) != hipSuccess || hipEventSynchronize(ev_meta) != hipSuccess)
+    return NVL_CRC32C_EHIP;
+  uint8_t v_meta = NVL_BLOCK_TRUNCATED;
+  std::vector<nvl_block_handle> meta_blocks;
+  std::vector<uint8_t> meta_bad;
+  if (meta_in) {
+    const uint8_t* mb = pin + p_meta;
+    v_meta = host_block_verdict(mb, meta_h.size);
+    if (v_meta == NVL_BLOCK_OK && mb[meta_h.size] == 0) block_handles(mb, meta_h.size, &meta_blocks, &meta_bad);
+  }
+  const uint64_t nm = meta_blocks.size(), n = nr + np + nm, cnt = 2 + nm + nr;
+  if (nm > nm_max || cnt > cap) {  // (nm_max bounds it) / the generic walk reports ENOSPC
+    (void)hipStreamSynchronize(st);
+    return NVL_CRC32C_OK;
+  }
+
+  // 4. meta slots, then ONE batch over data blocks + index pieces + meta blocks
+  uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
+  uint8_t* mv = pin + p_slots + nm * 16;
+  for (uint64_t j = 0; j < nm; ++j) {
+    const nvl_block_handle& b = meta_blocks[j];
+    const bool fits = !meta_bad[j] && block_in_file(b, len);
+    ms[j] = b.offset;
+    ms[nm + j] = fits ? b.size + 1 : 0;
+    mv[j] = meta_bad[j] ? (uint8_t)NVL_BLOCK_BAD_HANDLE : (fits ? kCompute : (uint8_t)NVL_BLOCK_TRUNCATED);
+  }
+  const uint64_t m0 = nr + np;
+  if (nm && (hipMemcpyAsync(boff + m0, ms, nm * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+             hipMemcpyAsync(blen + m0, ms + nm, nm * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+             hipMemcpyAsync(vk + m0, mv, nm, hipMemcpyHostToDevice, st) != hipSuccess))
+    return NVL_CRC32C_EHIP;
+  int rc = nvl_crc32c_batch_dev(f, boff, blen, nullptr, 0, crc, n, 0, ws, nvl_crc32c_batch_workspace_bytes(n), st);
+  if (rc != NVL_CRC32C_OK) return rc;
+  const size_t res_bytes = kResHead + 4 * np + nm;
+  uint8_t* res = pin + p_res;
+  if (launch_table_verdicts(f, boff, blen, crc, n, (uint32_t)nr, (uint32_t)np, vk, dres, st) != hipSuccess ||
+      hipMemcpyAsync(res, dres, res_bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return NVL_CRC32C_EHIP;
+  // the records, on the side stream once the parse has written them
+  if (hipStreamWaitEvent(side, ev_parse, 0) != hipSuccess ||
+      hipMemcpyAsync(blocks + 2 + nm, rec, nr * sizeof(nvl_table_block), hipMemcpyDeviceToHost, side) != hipSuccess)
+    return NVL_CRC32C_EHIP;
+  const hipError_t e1 = hipStreamSynchronize(st), e2 = hipStreamSynchronize(side);
+  if (e1 != hipSuccess || e2 != hipSuccess) return NVL_CRC32C_EHIP;
+
+  // 5. the index block's own check (Table::Open, table.cc:58-66) from its pieces
+  uint32_t bad;
+  uint64_t nb, nfix;
+  memcpy(&bad, res, 4);
+  memcpy(&nb, res + 8, 8);
+  memcpy(&nfix, res + 16, 8);
+  static const PieceFold pf;
+  const uint32_t* pc = reinterpret_cast<const uint32_t*>(res + kResHead);
+  const bool index_ok = pf.fold(pc, np, ilen) == unmask(le32(tail + 5));
+  if (bad || !index_ok) return NVL_CRC32C_OK;  // not the walk's list, or the index fails: generic
+  if (nfix) {  // some data block failed its check: its verdict replaces the record's OK
+    std::vector<uint8_t> v(nr);
+    if (hipMemcpyAsync(v.data(), vk, nr, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return NVL_CRC32C_EHIP;
+    for (uint64_t i = 0; i < nr; ++i) blocks[2 + nm + i].verdict = v[i];
+  }
+  blocks[0] = nvl_table_block{index_h.offset, index_h.size, NVL_TBLOCK_INDEX, NVL_BLOCK_OK};
+  blocks[1] = nvl_table_block{meta_h.offset, meta_h.size, NVL_TBLOCK_METAINDEX, v_meta};
+  const uint8_t* mvr = res + kResHead + 4 * np;
+  for (uint64_t j = 0; j < nm; ++j)
+    blocks[2 + j] = nvl_table_block{meta_blocks[j].offset, meta_blocks[j].size, NVL_TBLOCK_META, mvr[j]};
+  *n_blocks = cnt;
+  *table_status = NVL_TABLE_OK;
+  if (n_bad) *n_bad = nb + (v_meta != NVL_BLOCK_OK);
+  *done = true;
+  return NVL_CRC32C_OK;
+}
 
 }  // namespace
 }  // namespace nvl
@@ -78,10 +271,15 @@ int nvl_sstable_verify_table_dev(const void* file, uint64_t file_len, nvl_table_
   if (n_blocks) *n_blocks = 0;
   if (n_bad) *n_bad = 0;
   if ((!file && file_len) || !n_blocks || !table_status) return NVL_CRC32C_EINVAL;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  bool done = false;
+  const int rc = nvl::table_fast(static_cast<const uint8_t*>(file), file_len, blocks, cap, n_blocks, table_status,
+                                 n_bad, st, &done);
+  if (rc != NVL_CRC32C_OK || done) return rc;
   nvl::DeviceTable src;
   src.f = static_cast<const uint8_t*>(file);
   src.len = file_len;
-  src.st = static_cast<hipStream_t>(stream);
+  src.st = st;
   return nvl::verify_table_core(src, file_len, blocks, cap, n_blocks, table_status, n_bad);
 }
 

@@ -36,6 +36,18 @@ def handle(off: int, size: int) -> bytes:
     return varint(off) + varint(size)
 
 
+def _varint_handle(v: bytes) -> tuple[int, int]:
+    """handle() decoded back -> (offset, size)."""
+    out, shift, acc = [], 0, 0
+    for c in v:
+        acc |= (c & 127) << shift
+        shift += 7
+        if c < 128:
+            out.append(acc)
+            acc, shift = 0, 0
+    return out[0], out[1]
+
+
 def varint32_wrapped(x: int) -> bytes:
     """x < 2^28 as a 5-byte varint whose last byte carries bit 32: the
     reference's GetVarint32PtrFallback (util/coding.cc:112-129) accumulates

@@ -182,6 +182,59 @@ def test_table_cases_golden_device_resident(L, port):
         assert verify_dev(L, img) == tc.expected(c["trace"]), c["name"]
 
 
+def _indexed_table(port, nblocks, interval, damage, seed):
+    """A table of nblocks data blocks (1..2000 B, type 0/1), a filter block,
+    the metaindex and an index block with the given restart interval (1: the
+    TableBuilder form the GPU index parse reads; 2: prefix-compressed keys,
+    which it hands to the sequential walk).  damage: a few index values that
+    are no handle / point past the end, and flipped or retyped blocks."""
+    rng = np.random.default_rng(seed)
+    w = tc._Writer(port)
+    pool = rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes()
+    ents = []
+    for b in range(nblocks):
+        n = int(rng.integers(1, 2000))
+        s = int(rng.integers(0, len(pool) - n))
+        h = w.raw(pool[s:s + n], int(rng.integers(0, 2)))
+        key = b"user-key-%012d" % b + (b"~" * 150 if b % 97 == 5 else b"")  # some keys need 2-byte varints
+        ents.append((key, tc.handle(*h)))
+    filt = w.raw(pool[:777])
+    meta_h = w.raw(tc.block([(b"filter.leveldb.BuiltinBloomFilter2", tc.handle(*filt))], 16))
+    flips = []
+    if damage:
+        ents[5] = (ents[5][0], b"\xff")                               # not a BlockHandle
+        ents[7] = (ents[7][0], tc.handle(len(w.img) + 1000, 10))      # past the end
+        flips = sorted(set(int(x) for x in rng.integers(10, nblocks, 40)))
+    idx = tc.block(ents, interval)
+    index_h = w.raw(idx)
+    foot = tc.handle(*meta_h) + tc.handle(*index_h)
+    w.img += foot + bytes(40 - len(foot)) + tc.MAGIC.to_bytes(8, "little")
+    img = bytearray(w.img)
+    for b in flips:  # flip a content byte or the type byte of data block b
+        off, n = tc._varint_handle(ents[b][1])
+        img[off + (int(rng.integers(0, n)) if b % 3 else n)] ^= 0x40
+    return bytes(img), len(flips)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("interval,damage", [(1, False), (1, True), (2, False), (2, True)])
+def test_table_dev_index_parse_at_size(L, port, interval, damage):
+    """A 20000-block table through nvl_sstable_verify_table_dev: the GPU
+    index parse (interval 1) and the sequential fallback (interval 2) both
+    give the host walk's list (NVL_FRAMING_HOST) exactly, clean and damaged."""
+    if not gpu_present():
+        pytest.skip("no GPU")
+    img, nflip = _indexed_table(port, 20_000, interval, damage, 17 + interval)
+    want = verify(L, img, HOST)
+    got = verify_dev(L, img)
+    assert got[0] == want[0] == 0
+    assert len(got[1]) == len(want[1]) == 20_000 + 3
+    bad = [i for i, (a, b) in enumerate(zip(got[1], want[1])) if a != b]
+    assert not bad, (bad[:5], [got[1][i] for i in bad[:5]], [want[1][i] for i in bad[:5]])
+    data_bad = sum(b[3] != 0 for b in want[1] if b[2] == 3)
+    assert data_bad == (nflip + 2 if damage else 0)
+
+
 def test_table_verify_dev_arguments(L):
     lib = L.lib
     n = ctypes.c_size_t(7)

@@ -1833,7 +1833,11 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       for (int o = 32; o > 0; o >>= 1) mj = max(mj, (uint32_t)__shfl_xor((int)mj, o));
       if (lane == 63) wsum[wv] = x;
       if (lane == 0) wmax[wv] = mj;
-      __syncthreads();  // (also: the tables are in LDS)
+      // (also: the tables are in LDS, and wave 0's zeroing of the list
+      // counters ctl is ordered before every wave's list appends -- without
+      // this barrier an append could land first: round 3 faulted a parity
+      // test that way)
+      __syncthreads();
       // the 16 waves' totals and flags across lanes 0..15 (a wave scan, not
       // 48 LDS reads held in registers at once)
       const bool lw = (uint32_t)lane < kWavesPerWG;

@@ -490,8 +490,11 @@ struct VarGeom {
 // (every chunk full, no masking: configs 2, 4, 5); kGeneral = the full
 // 4096-byte chunks of buffers of any alignment and length (realignment).
 // Partial first chunks (heads) never reach these kernels: crc32c_head_kernel
-// runs them, so the body kernels' registers never hold masking code.
-enum LoadMode : int { kAligned = 0, kGeneral = 1 };
+// runs them, so the body kernels' registers never hold masking code -- except
+// kMasked: fixed-stride batches of one 1025..4095-byte chunk per buffer, none
+// starting in a page's first 16-byte granule (launch_fixed checks), run as
+// long heads (load_general / realign_general with hd) under scheduler A.
+enum LoadMode : int { kAligned = 0, kGeneral = 1, kMasked = 2 };
 
 // Bytes of a buffer's first chunk (END-aligned chunks: the only short one).
 __host__ __device__ __forceinline__ uint32_t head_bytes(uint64_t L, uint32_t J) {
@@ -581,7 +584,7 @@ __device__ __forceinline__ void load_chunk(const BufInfo& bi, uint32_t c, int la
       ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
     }
   } else {
-    load_general(ce, false, (uintptr_t)bi.p, lane, ch);
+    load_general(ce, M == kMasked, (uintptr_t)bi.p, lane, ch);
   }
 }
 
@@ -700,7 +703,7 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
     if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0, word 0
   } else {
     (void)ov;
-    realign_general(chunk_end(bi, c), false, (uintptr_t)bi.p, bi.s, lane, ch, w);
+    realign_general(chunk_end(bi, c), M == kMasked, (uintptr_t)bi.p, bi.s, lane, ch, w);
   }
 }
 
@@ -2066,6 +2069,14 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
       run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
       return;
     }
+    // one partial chunk per buffer, 1025..4095 bytes, no start in a page's
+    // first granule (launch_fixed's masked_pairs): each buffer a long head,
+    // in scheduler A's order (10^5 x 3500 B at stride 4128: 75.3 -> 71.3 us
+    // against the head kernel, profiles/r03_ablations)
+    if (g.J == 1) {
+      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kMasked>(g, ka, lds);
+      return;
+    }
   }
 #endif
   if constexpr (M == kGeneral) run_general<waves_of<M>()>(g, ka, lds);
@@ -2770,6 +2781,20 @@ size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
   return r + (hcs ? n * sizeof(uint32_t) : 0);
 }
 
+// True when no buffer start base + k stride (k < n) lies in the first 16-byte
+// granule of a 4 KiB page: the long-head loads (load_general with hd) read up
+// to 12 bytes below a start's granule, inside its page only then.  The starts
+// mod 4096 step by d = stride mod 4096; past one period (4096 / gcd(d, 4096)
+// steps) they are every residue = base mod gcd.
+static bool starts_off_page_heads(const uint8_t* base, uint64_t stride, uint64_t n) {
+  const uint64_t b = (uintptr_t)base & 4095u, d = stride & 4095u;
+  const uint64_t gd = d ? (d & (~d + 1u)) : 4096u;  // gcd(d, 4096): d's lowest set bit
+  if (n >= 4096u / gd) return b % gd >= 16u;
+  for (uint64_t k = 0, r = b; k < n; ++k, r = (r + d) & 4095u)
+    if (r < 16u) return false;
+  return true;
+}
+
 hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
                         const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* ws) {
   if (n == 0) return hipSuccess;
@@ -2778,7 +2803,8 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   const bool aligned = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
   Rec* recs = J > 1 ? ws : nullptr;
-  const bool heads = !aligned && dev::head_first(len);  // every buffer's first chunk is a head chunk
+  const bool masked = !aligned && J == 1 && len >= 1025 && len < dev::kChunk && starts_off_page_heads(base, stride, n);
+  const bool heads = !aligned && dev::head_first(len) && !masked;  // every buffer's first chunk is a head chunk
   // Short mode (run_heads): two-chunk buffers with a 1..3-byte head (block |
   // type of 4096-byte blocks at a fixed stride) are finished by the head
   // kernel, body chunk and all; no masked head can start a page there.

@@ -428,3 +428,39 @@ def test_fixed_chunk_parallel(dev, C, port, J, n, gap):
     got = _u32(C.extend_fixed(buf, stride, L, n, 0x0BADF00D, mask=True))
     want = port.fixed(host, stride, L, n, np.full(n, 0x0BADF00D, dtype=np.uint32))
     assert np.array_equal(got, np.array([port.mask(int(x)) for x in want], dtype=np.uint32))
+
+
+def _page_head_start(base_off, stride, n):
+    """Some start base_off + k stride (k < n), offsets from a page start, in
+    a page's first 16 bytes."""
+    return any(((base_off + k * stride) & 4095) < 16 for k in range(n))
+
+
+@pytest.mark.parametrize("length", [1025, 1500, 2049, 3500, 4095])
+@pytest.mark.parametrize("layout", ["clear", "page_heads"])
+def test_fixed_masked_pairs(dev, C, port, length, layout):
+    """Fixed-stride batches of one 1025..4095-byte chunk per buffer: with no
+    start in a page's first granule they run as masked scheduler-A passes
+    (crc32c_fixed_kernel<kGeneral>, kMasked), otherwise through the head
+    kernel; per-buffer inits and Mask, odd strides and bases."""
+    if layout == "clear":
+        base_off, stride = 48, (length + 31) // 32 * 32 + 4096 * ((length // 2048) % 2)
+        if stride % 4096 == 0:
+            stride += 32
+    else:
+        base_off, stride = 5, length + 3
+    n = 20000
+    assert _page_head_start(base_off, stride, n) == (layout == "page_heads")
+    rng = np.random.default_rng(length * 7 + len(layout))
+    total = 4096 + base_off + (n - 1) * stride + length + 64
+    host = port.fill(int(rng.integers(1, 1 << 40)), 0, total)
+    buf = torch.from_numpy(host).to(dev)
+    base_off += -buf.data_ptr() % 4096  # offsets relative to a page start
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    got = _u32(C.extend_fixed(buf, stride, length, n, torch.from_numpy(inits.view(np.int32)).to(dev),
+                              base_offset=base_off))
+    want = port.fixed(host[base_off:], stride, length, n, inits)
+    assert np.array_equal(got, want)
+    got = _u32(C.extend_fixed(buf, stride, length, n, 0x2468ACE1, base_offset=base_off, mask=True))
+    want = port.fixed(host[base_off:], stride, length, n, np.full(n, 0x2468ACE1, dtype=np.uint32))
+    assert np.array_equal(got, np.array([port.mask(int(x)) for x in want], dtype=np.uint32))

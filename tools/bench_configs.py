@@ -5,6 +5,7 @@ around each call, median of R reps), every result checked.
   v        10^5 x 4097 B at stride 4101: block | type of 4096-byte SSTable blocks with their
            4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
   g        10^5 x 4096 B at stride 4099 from an odd base: the fixed-stride general path
+  f        10^5 x 3500 B at stride 4128 from base 48: fixed-stride one-partial-chunk buffers
   r        10^5 buffers of 3364..4109 B (the n+1 of data blocks at block_size 4096)
            at stride length+4, nvl_crc32c_batch_dev
 v, g and r are checked CRC by CRC against the oracle."""
@@ -86,8 +87,10 @@ for c in a.configs.split(","):
         alg = int(lens.sum()) + 20 * n
         host = buf.cpu().numpy()
         check = lambda res: bool(np.array_equal(res, p.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64))))
-    elif c == "g":
-        n, L, S, off = 100_000, 4096, 4099, 3
+    elif c in ("g", "f"):
+        # g: 10^5 x 4096 B at stride 4099 from an odd base; f: 10^5 x 3500 B
+        # at stride 4128 from base 48 (one partial chunk per buffer, fixed stride)
+        n, L, S, off = (100_000, 4096, 4099, 3) if c == "g" else (100_000, 3500, 4128, 48)
         buf = torch.empty(off + n * S + 64, dtype=torch.uint8, device=dev)
         lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), buf.numel() // 8, 8, 0, 1, 0x5EED00B2, None)
         out = torch.empty(n, dtype=torch.int32, device=dev)

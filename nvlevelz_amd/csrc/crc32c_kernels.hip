@@ -1652,8 +1652,10 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
   // G::meta_addr; f = 4: hc[i] of a kTInj body), read out with v_readlane.
   // (Scalar metadata loads -- an s_load in flight makes every LDS wait of
   // the chains wait for it too, so they had to land, exposed, between the
-  // word build and the chains -- and a separate hc load: v 88.5 -> 86.8 us,
-  // r and config 3 unchanged, profiles/r03_ablations.  The metadata load
+  // word build and the chains -- and a separate hc load: v 85.2-87.4 vs
+  // 85.6-88.6 us over two boxes, r, f and config 3 unchanged -- within the
+  // noise, profiles/r03_ablations; the layout-computed metadata of the
+  // ablation saved ~5 us, so the load's cost is not all latency).  The load
   // must be issued before the chunk loads: between them and the chains the
   // compiler serialised the two chains, v 88.6 -> 99-104 us.)
   auto entries = [&](uint32_t k, uint32_t& t0, uint32_t& t1) {

@@ -221,7 +221,7 @@ int do_fixed(DeviceState* s, const void* base, uint64_t stride, uint64_t len, ui
 
 int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const uint64_t* lengths,
              const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags, void* ws,
-             size_t ws_bytes, hipStream_t st) {
+             size_t ws_bytes, hipStream_t st, uint64_t max_len = UINT64_MAX) {
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out) return NVL_CRC32C_EINVAL;
   if (n >= (1ull << 31) - 2) return NVL_CRC32C_EINVAL;
@@ -248,7 +248,7 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   if (s->num_cu <= 1023) lc.counter = counters_for(s, st);
   if (lc.counter) {  // (cs holds lpre, the unit map region the tiles)
     hipError_t ef = launch_var_fused(lc, static_cast<const uint8_t*>(base), offsets, lengths, n, init, init_all, out,
-                                     flags, recs, hc, cs, unit_first);
+                                     flags, recs, hc, cs, unit_first, max_len);
     if (own) (void)hipFreeAsync(ws, st);
     return hip_rc(ef);
   }
@@ -660,10 +660,11 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   DeviceState* s = current_state(&rc);
   if (!s) return rc;
   // host layout: [data (16-B aligned per buffer)] [offsets n] [lengths n] [init n]
-  uint64_t data_bytes = 0;
+  uint64_t data_bytes = 0, max_len = 0;  // (the lengths are on the host: a bound for the plan)
   for (uint64_t i = 0; i < n; ++i) {
     if (!ptrs[i] && lengths[i]) return NVL_CRC32C_EINVAL;
     data_bytes += align_up(lengths[i], 16);
+    max_len = std::max(max_len, lengths[i]);
   }
   const size_t meta_off = align_up(data_bytes, 256);
   const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
@@ -692,7 +693,7 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   hipError_t e = hipMemcpyAsync(d, hst, total, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
-                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);
+                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
   else
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
@@ -739,11 +740,12 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
                                  uint64_t n, uint32_t flags) {
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out || (!region && region_len)) return NVL_CRC32C_EINVAL;
-  uint64_t lo = UINT64_MAX, hi = 0;  // staged window [lo, hi)
+  uint64_t lo = UINT64_MAX, hi = 0, max_len = 0;  // staged window [lo, hi)
   for (uint64_t i = 0; i < n; ++i) {
     if (lengths[i] > region_len || offsets[i] > region_len - lengths[i]) return NVL_CRC32C_EINVAL;
     if (offsets[i] < lo) lo = offsets[i];
     if (offsets[i] + lengths[i] > hi) hi = offsets[i] + lengths[i];
+    max_len = std::max(max_len, lengths[i]);
   }
   int rc = NVL_CRC32C_OK;
   DeviceState* s = current_state(&rc);
@@ -778,7 +780,7 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   if (e == hipSuccess) e = hipMemcpyAsync(d + meta_off, hst + meta_off, total - meta_off, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
-                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);
+                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
   else
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));

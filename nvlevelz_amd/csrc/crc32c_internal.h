@@ -74,10 +74,16 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
 // A variable-length batch in two launches (lc.counter set): the head kernel
 // (heads + the plan's tiles: lpre[n], tiles[2 * head grid]) and the fused
 // kernel (chunk positions from the tiles, checksum, fix-up); recs: the
-// launch_var workspace records (hold the edge records).
+// launch_var workspace records (hold the edge records).  max_len: a bound
+// on the lengths the caller knows on the host (UINT64_MAX: none); when it
+// makes every tile a short-mode tile (see var_heads_only) the fused kernel,
+// which would return at once, is not launched.
 hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                             uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
-                            Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles);
+                            Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles, uint64_t max_len = UINT64_MAX);
+// The head kernel finishes every buffer of an n-buffer batch whose lengths
+// are all <= max_len: two chunks at most, one sub-range per tile.
+bool var_heads_only(int num_cu, uint64_t n, uint64_t max_len);
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

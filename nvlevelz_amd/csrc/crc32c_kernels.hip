@@ -2911,14 +2911,21 @@ size_t var_unit_map_bytes(int num_cu) { return (uint64_t)num_cu * dev::kUnitsPer
 
 bool var_plan_small(uint64_t n) { return n <= dev::kPlanSmallMax; }
 
+// Short mode (run_heads) needs a tile's largest chunk count <= 2 and the
+// tile scan fused into the classification (a tile of <= kHeadSub buffers).
+bool var_heads_only(int num_cu, uint64_t n, uint64_t max_len) {
+  const uint64_t G = head_grid(num_cu, n);
+  return max_len <= 2ull * dev::kChunk && (n + G - 1) / G <= dev::kHeadSub;
+}
+
 hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths,
                             uint64_t n, const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags,
-                            Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles) {
+                            Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles, uint64_t max_len) {
   if (n == 0) return hipSuccess;
   if (!lc.counter || !lpre || !tiles || lc.num_cu > (int)dev::kMaxTiles) return hipErrorInvalidValue;
   dev::VarGeom g{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
   hipError_t eh = launch_heads(lc, g, out, flags, hc, nullptr, lpre, tiles, /*short_ok=*/true);
-  if (eh != hipSuccess) return eh;
+  if (eh != hipSuccess || var_heads_only(lc.num_cu, n, max_len)) return eh;
   dev::KArgs ka{out, flags, recs, lc.tables, lc.counter, hc};
   ka.lpre = lpre;
   ka.tiles = tiles;

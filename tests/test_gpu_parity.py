@@ -464,3 +464,39 @@ def test_fixed_masked_pairs(dev, C, port, length, layout):
     got = _u32(C.extend_fixed(buf, stride, length, n, 0x2468ACE1, base_offset=base_off, mask=True))
     want = port.fixed(host[base_off:], stride, length, n, np.full(n, 0x2468ACE1, dtype=np.uint32))
     assert np.array_equal(got, np.array([port.mask(int(x)) for x in want], dtype=np.uint32))
+
+
+@pytest.mark.parametrize("n,maxlen", [(1, 8192), (5000, 8192), (5000, 8193), (1_200_000, 300)])
+def test_region_host_short_batches(dev, C, port, n, maxlen):
+    """nvl_crc32c_batch_region_host knows the lengths on the host: when every
+    length is <= 8192 (two chunks) and the tiles are small enough for the head
+    kernel's short mode, the fused body kernel is not launched at all
+    (var_heads_only); 8193 and 1.2M buffers (tiles past one sub-range) keep
+    both launches.  Lengths 0..3, 4096..4099 and maxlen itself, starts in a
+    page's first granule included."""
+    from nvlevelz_amd import _lib
+    rng = np.random.default_rng(n + maxlen)
+    lens = rng.integers(0, maxlen + 1, size=n).astype(np.uint64)
+    special = np.array([0, 1, 2, 3, 4, 4095, 4096, 4097, 4098, 4099, maxlen], dtype=np.uint64)
+    special = special[special <= maxlen]
+    k = min(n, special.size)
+    lens[:k] = special[:k]
+    lens[-1] = maxlen
+    gaps = rng.integers(0, 20, size=n).astype(np.uint64)
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 4096 * 3  # buffer 0 at a page start
+    for i in range(n):
+        offs[i] = pos
+        pos += int(lens[i] + gaps[i])
+    region = port.fill(0x5A + n, 0, pos + 64)
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    out = np.zeros(n, dtype=np.uint32)
+    rc = _lib.lib.nvl_crc32c_batch_region_host(region.ctypes.data, region.nbytes, offs.ctypes.data, lens.ctypes.data,
+                                               inits.ctypes.data, 0, out.ctypes.data, n, 1)
+    assert rc == 0, rc
+    want = port.varlen(region, offs, lens, inits)
+    assert np.array_equal(out, np.array([port.mask(int(x)) for x in want], dtype=np.uint32))
+    if n <= 5000:  # nvl_crc32c_batch_host: the same buffers packed by the library, 16-B aligned starts
+        blobs = [region[int(o):int(o) + int(m)].tobytes() for o, m in zip(offs, lens)]
+        got = C.extend_batch_host(blobs, [int(x) for x in inits])
+        assert np.array_equal(np.asarray(got, dtype=np.uint32), want)

@@ -502,9 +502,9 @@ struct VarGeom {
 // 4096-byte chunks of buffers of any alignment and length (realignment).
 // Partial first chunks (heads) never reach these kernels: crc32c_head_kernel
 // runs them, so the body kernels' registers never hold masking code -- except
-// kMasked: fixed-stride batches of one 1025..4095-byte chunk per buffer, none
-// starting in a page's first 16-byte granule (launch_fixed checks), run as
-// long heads (load_general / realign_general with hd) under scheduler A.
+// kMasked: fixed-stride batches of one 1025..4095-byte chunk per buffer, run
+// as long heads (load_general / realign_general with hd, page_head_words)
+// under scheduler A.
 enum LoadMode : int { kAligned = 0, kGeneral = 1, kMasked = 2 };
 
 // Bytes of a buffer's first chunk (END-aligned chunks: the only short one).
@@ -550,11 +550,13 @@ __device__ __forceinline__ uint32_t lane_load_off(int lane) {
 //   body chunk (hd false: cs >= p): rows from A4 = cs rounded down to 4 B
 //     (gfx950 serves 4-B aligned dwordx4 at the 16-B aligned rate,
 //     byte-misaligned at ~2/3: tools/diag/ldpat.hip); A4 >= floor4(p) >= g.
-//   head chunk (hd: crc32c_head_kernel's long heads, cs < p): rows from A4
-//     as well; a row slot wholly below p's granule g is loaded from g instead
-//     (its bytes precede the buffer and are masked).  The slot straddling g
-//     reads up to 12 bytes below g: the caller guarantees g is not the first
-//     granule of a 4 KiB page, so they are in g's page (mapped).
+//   head chunk (hd: crc32c_head_kernel's long heads, kMasked passes, cs < p):
+//     rows from A4 as well; a row slot wholly below p's granule g is loaded
+//     from g instead (its bytes precede the buffer and are masked).  The slot
+//     straddling g reads up to 12 bytes below g, inside g's 4 KiB page --
+//     unless g is the page's first granule: then it is loaded from g too and
+//     page_head_words moves its words into place (kMasked; the head kernel
+//     sends such heads to lane-group rounds instead).
 // The edge load is the dword holding byte ce - 1 (lane 63's dword past its
 // row data when the body rows start below cs).  Fault safety: only 16-B
 // granules that hold buffer bytes are touched (tests/kernel_model.py).  The
@@ -566,10 +568,11 @@ __device__ __forceinline__ void load_general(uintptr_t ce, bool hd, uintptr_t p,
   uintptr_t a[4];
   if (hd) {
     const uintptr_t A4 = cs & ~(uintptr_t)3, g = p & ~(uintptr_t)15;
+    const uintptr_t gl = (g & 4095u) ? g - 15u : g;  // below gl: loaded from g
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uintptr_t x = A4 + 1024u * (uint32_t)j + lo;
-      a[j] = x + 16u <= g ? g : x;
+      a[j] = x < gl ? g : x;
     }
   } else {
     const uintptr_t A4 = cs & ~(uintptr_t)3;
@@ -582,6 +585,30 @@ __device__ __forceinline__ void load_general(uintptr_t ce, bool hd, uintptr_t p,
     ch.d[4 * j + 0] = v.x; ch.d[4 * j + 1] = v.y; ch.d[4 * j + 2] = v.z; ch.d[4 * j + 3] = v.w;
   }
   ch.e[3] = *(const __attribute__((address_space(1))) uint32_t*)((ce - 1u) & ~(uintptr_t)3);
+}
+
+// A kMasked pass whose buffer starts in a page's first granule g: the row
+// slot straddling g was loaded from g (load_general), so its words move up by
+// q = (g - x) / 4 dwords to sit at their chunk positions (the words below g
+// precede the buffer: head_fix zeroes them).  Wave-uniform branch, taken by
+// ~1/256 of random starts.
+__device__ __forceinline__ void page_head_words(uintptr_t ce, uintptr_t p, int lane, uint32_t (&w)[16]) {
+  const uintptr_t g = p & ~(uintptr_t)15;
+  if (g & 4095u) return;
+  const uintptr_t A4 = (ce - kChunk) & ~(uintptr_t)3;
+  const uint32_t lo = lane_load_off(lane);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uintptr_t x = A4 + 1024u * (uint32_t)j + lo;
+    const bool st = x < g && x + 16u > g;
+    const uint32_t q = (uint32_t)(g - x) >> 2;  // 1..3 when st
+    const uint32_t x0 = w[4 * j], x1 = w[4 * j + 1], x2 = w[4 * j + 2];
+    if (st) {
+      w[4 * j + 3] = q == 1u ? x2 : (q == 2u ? x1 : x0);
+      w[4 * j + 2] = q == 1u ? x1 : x0;
+      w[4 * j + 1] = x0;
+    }
+  }
 }
 
 template <int M>
@@ -709,6 +736,7 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
                                             uint32_t (&w)[16], uint32_t (&ov)[4]) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) w[k] = ch.d[k];
+  if constexpr (M == kMasked) page_head_words(chunk_end(bi, c), (uintptr_t)bi.p, lane, w);
   row_transpose(w);
   if constexpr (M == kAligned) {
     if (c == 0 && lane == 0) w[0] ^= bi.s;  // chunk position 0 is lane 0, word 0
@@ -2107,10 +2135,9 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
       run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
       return;
     }
-    // one partial chunk per buffer, 1025..4095 bytes, no start in a page's
-    // first granule (launch_fixed's masked_pairs): each buffer a long head,
-    // in scheduler A's order (10^5 x 3500 B at stride 4128: 75.3 -> 71.3 us
-    // against the head kernel, profiles/r03_ablations)
+    // one partial chunk per buffer, 1025..4095 bytes (launch_fixed): each
+    // buffer a long head, in scheduler A's order (10^5 x 3500 B at stride
+    // 4128: 75.3 -> 71.3 us against the head kernel, profiles/r03_ablations)
     if (g.J == 1) {
       run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kMasked>(g, ka, lds);
       return;
@@ -2819,20 +2846,6 @@ size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
   return r + (hcs ? n * sizeof(uint32_t) : 0);
 }
 
-// True when no buffer start base + k stride (k < n) lies in the first 16-byte
-// granule of a 4 KiB page: the long-head loads (load_general with hd) read up
-// to 12 bytes below a start's granule, inside its page only then.  The starts
-// mod 4096 step by d = stride mod 4096; past one period (4096 / gcd(d, 4096)
-// steps) they are every residue = base mod gcd.
-static bool starts_off_page_heads(const uint8_t* base, uint64_t stride, uint64_t n) {
-  const uint64_t b = (uintptr_t)base & 4095u, d = stride & 4095u;
-  const uint64_t gd = d ? (d & (~d + 1u)) : 4096u;  // gcd(d, 4096): d's lowest set bit
-  if (n >= 4096u / gd) return b % gd >= 16u;
-  for (uint64_t k = 0, r = b; k < n; ++k, r = (r + d) & 4095u)
-    if (r < 16u) return false;
-  return true;
-}
-
 hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t stride, uint64_t len, uint64_t n,
                         const uint32_t* init, uint32_t init_all, uint32_t* out, uint32_t flags, Rec* ws) {
   if (n == 0) return hipSuccess;
@@ -2841,7 +2854,7 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   const bool aligned = len > 0 && (len % dev::kChunk) == 0 && ((uintptr_t)base % 16) == 0 && (stride % 16) == 0;
   dev::FixedGeom g{base, stride, len, n, J, init, init_all};
   Rec* recs = J > 1 ? ws : nullptr;
-  const bool masked = !aligned && J == 1 && len >= 1025 && len < dev::kChunk && starts_off_page_heads(base, stride, n);
+  const bool masked = !aligned && J == 1 && len >= 1025 && len < dev::kChunk;
   const bool heads = !aligned && dev::head_first(len) && !masked;  // every buffer's first chunk is a head chunk
   // Short mode (run_heads): two-chunk buffers with a 1..3-byte head (block |
   // type of 4096-byte blocks at a fixed stride) are finished by the head

@@ -237,6 +237,49 @@ def long_head_raw(mem: bytes, p: int, L: int, J: int, s: int) -> int:
     return wave_fold(lanes)
 
 
+def masked_pass_raw(mem: bytes, p: int, L: int, s: int) -> int:
+    """Raw register of a one-chunk buffer of 1025..4095 bytes as a kMasked
+    scheduler-A pass (crc32c_fixed_kernel<kGeneral>: load_general with hd,
+    page_head_words, realign_general with hd), at ANY start: the row slot
+    straddling p's granule g reads up to 12 bytes below g -- unless g is a
+    page's first granule, where it is loaded from g and its words are moved up
+    by (g - x) / 4 dwords.  Fault safety: below g only inside g's page."""
+    assert 1025 <= L < CHUNK
+    ce = p + L
+    cs = ce - CHUNK
+    g = p & ~15
+    A4 = cs & ~3
+    r = cs & 3
+    gl = g - 15 if g & 4095 else g
+
+    def load(a: int, n: int) -> bytes:
+        assert ((a + n - 1) & ~15) <= ((ce - 1) & ~15), (a, n, p, ce)
+        assert (a & ~15) >= g or (a >> 12) == (g >> 12), (a, n, p, g)
+        return mem[a:a + n]
+
+    data = bytearray(CHUNK + 4)
+    for k in range(CHUNK // 16):
+        x = A4 + 16 * k
+        slot = bytearray(load(g if x < gl else x, 16))
+        if not g & 4095 and x < g < x + 16:  # page_head_words
+            q = (g - x) // 4
+            slot = bytearray(4 * q) + slot[:16 - 4 * q]
+        data[16 * k:16 * k + 16] = slot
+    data[CHUNK:CHUNK + 4] = load((ce - 1) & ~3, 4)
+    piece = bytearray(data[r:r + CHUNK])
+    rel = p - cs
+    piece[:rel] = bytes(rel)
+    for q in range(4):
+        piece[rel + q] ^= (s >> (8 * q)) & 0xFF
+    lanes = []
+    for lane in range(64):
+        crc = 0
+        for k in range(16):
+            crc = slice4(crc ^ int.from_bytes(piece[64 * lane + 4 * k:64 * lane + 4 * k + 4], "little"))
+        lanes.append(crc)
+    return wave_fold(lanes)
+
+
 def chunk_raw(mem: bytes, p: int, L: int, J: int, c: int, s: int) -> int:
     """Raw register of chunk c of buffer [p, p+L) with ~init = s injected,
     computed the way load_chunk<kGeneral> / build_words<kGeneral> do it (a

@@ -152,3 +152,21 @@ def test_long_head_model(port, page_off):
         got = km.chunk_raw(mem, p, L, J, 0, s)
         assert got == km.raw_bytes(0, bytes(4096 - hl) + bytes(b ^ ((s >> (8 * q)) & 0xFF) if q < 4 else b
                                                               for q, b in enumerate(mem[p:p + hl]))), (p, hl)
+
+
+@pytest.mark.parametrize("page_off", [0, 1, 4, 13, 15, 16, 17, 28, 4079, 4080])
+def test_masked_pass_model(port, page_off):
+    """kMasked scheduler-A passes (fixed batches of one 1025..4095-byte chunk
+    per buffer) at starts around a 4 KiB page boundary, page-first granules
+    included (page_head_words): loads stay in the buffer's granules or in its
+    first granule's page, and the register matches the reference."""
+    mem = bytes(port.fill(0x3A5C, 0, 64 * 4096))
+    rng = random.Random(1000 + page_off)
+    for k in range(30):
+        L = rng.choice([1025, 1026, 1027, 1028, 1100, 2047, 2048, 2049, 3000, 3500, 4000, 4080, 4092, 4095])
+        p = 4096 * (2 + 13 * k % 40) + page_off
+        s = rng.getrandbits(32)
+        got = km.masked_pass_raw(mem, p, L, s)
+        want = km.raw_bytes(0, bytes(4096 - L) + bytes(b ^ ((s >> (8 * q)) & 0xFF) if q < 4 else b
+                                                       for q, b in enumerate(mem[p:p + L])))
+        assert got == want, (p, L)

@@ -6,6 +6,7 @@ around each call, median of R reps), every result checked.
            4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
   g        10^5 x 4096 B at stride 4099 from an odd base: the fixed-stride general path
   f        10^5 x 3500 B at stride 4128 from base 48: fixed-stride one-partial-chunk buffers
+  q        10^5 x 3500 B packed at stride 3500: the same, some starts in a page's first granule
   r        10^5 buffers of 3364..4109 B (the n+1 of data blocks at block_size 4096)
            at stride length+4, nvl_crc32c_batch_dev
 v, g and r are checked CRC by CRC against the oracle."""
@@ -87,10 +88,13 @@ for c in a.configs.split(","):
         alg = int(lens.sum()) + 20 * n
         host = buf.cpu().numpy()
         check = lambda res: bool(np.array_equal(res, p.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64))))
-    elif c in ("g", "f"):
+    elif c in ("g", "f", "q"):
         # g: 10^5 x 4096 B at stride 4099 from an odd base; f: 10^5 x 3500 B
-        # at stride 4128 from base 48 (one partial chunk per buffer, fixed stride)
-        n, L, S, off = (100_000, 4096, 4099, 3) if c == "g" else (100_000, 3500, 4128, 48)
+        # at stride 4128 from base 48 (one partial chunk per buffer, fixed
+        # stride); q: 10^5 x 3500 B packed (stride 3500, some starts in a
+        # page's first granule)
+        n, L, S, off = {"g": (100_000, 4096, 4099, 3), "f": (100_000, 3500, 4128, 48),
+                        "q": (100_000, 3500, 3500, 0)}[c]
         buf = torch.empty(off + n * S + 64, dtype=torch.uint8, device=dev)
         lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), buf.numel() // 8, 8, 0, 1, 0x5EED00B2, None)
         out = torch.empty(n, dtype=torch.int32, device=dev)

@@ -1705,7 +1705,7 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
     }
     return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)a);
   };
-  auto rl = [](uint32_t v, int l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); };
+  auto rl = [](uint32_t v, uint32_t l) -> uint32_t { return lane_u32(v, l); };
   // positions of one entry; for a PAIR slot the first pass is the head, the
   // second the body
   auto pos = [&](uint64_t o, uint32_t L, uint32_t s, uint32_t tag, bool second, SlotPass& q) {

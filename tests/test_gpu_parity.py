@@ -500,3 +500,21 @@ def test_region_host_short_batches(dev, C, port, n, maxlen):
         blobs = [region[int(o):int(o) + int(m)].tobytes() for o, m in zip(offs, lens)]
         got = C.extend_batch_host(blobs, [int(x) for x in inits])
         assert np.array_equal(np.asarray(got, dtype=np.uint32), want)
+
+
+@pytest.mark.parametrize("length,stride,n", [(1025, 1, 5000), (3000, 7, 3000), (4095, 1000, 2000), (2049, 4096, 3),
+                                             (3500, 3500, 1), (1100, 16, 2)])
+def test_fixed_masked_pairs_overlapping(dev, C, port, length, stride, n):
+    """kMasked scheduler-A passes over fixed batches whose buffers overlap
+    (stride < len, down to 1 byte: every start alignment and, with a page-
+    aligned base, starts in pages' first granules), and tiny n."""
+    rng = np.random.default_rng(length * 131 + stride)
+    total = 4096 + (n - 1) * stride + length + 64
+    host = port.fill(int(rng.integers(1, 1 << 40)), 0, total)
+    buf = torch.from_numpy(host).to(dev)
+    base_off = -buf.data_ptr() % 4096  # the first buffer at a page start
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    got = _u32(C.extend_fixed(buf, stride, length, n, torch.from_numpy(inits.view(np.int32)).to(dev),
+                              base_offset=base_off))
+    want = port.fixed(host[base_off:], stride, length, n, inits)
+    assert np.array_equal(got, want)

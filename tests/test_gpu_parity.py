@@ -439,10 +439,11 @@ def _page_head_start(base_off, stride, n):
 @pytest.mark.parametrize("length", [1025, 1500, 2049, 3500, 4095])
 @pytest.mark.parametrize("layout", ["clear", "page_heads"])
 def test_fixed_masked_pairs(dev, C, port, length, layout):
-    """Fixed-stride batches of one 1025..4095-byte chunk per buffer: with no
-    start in a page's first granule they run as masked scheduler-A passes
-    (crc32c_fixed_kernel<kGeneral>, kMasked), otherwise through the head
-    kernel; per-buffer inits and Mask, odd strides and bases."""
+    """Fixed-stride batches of one 1025..4095-byte chunk per buffer run as
+    masked scheduler-A passes (crc32c_fixed_kernel<kGeneral>, kMasked):
+    layouts with no start in a page's first granule, and layouts with such
+    starts (page_head_words moves the straddling slot's words); per-buffer
+    inits and Mask, odd strides and bases."""
     if layout == "clear":
         base_off, stride = 48, (length + 31) // 32 * 32 + 4096 * ((length // 2048) % 2)
         if stride % 4096 == 0:

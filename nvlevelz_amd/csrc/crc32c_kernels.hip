@@ -369,17 +369,11 @@ struct FixedGeom {
   __device__ __forceinline__ uint64_t offsets_at(uint64_t i) const { return i * stride; }
   __device__ __forceinline__ uint64_t lengths_at(uint64_t) const { return len; }
   __device__ __forceinline__ uint32_t lengths_lo(uint64_t) const { return (uint32_t)len; }
-  // drain_list's vector metadata: the dword to load for field f (0, 1:
-  // offset, 2: length's low word, 3: init) of buffer i, or `safe`; then the
-  // fields from the loaded dwords x[]
-  __device__ __forceinline__ uintptr_t meta_addr(uint64_t i, uint32_t f, uintptr_t safe) const {
-    return f == 3u && init ? (uintptr_t)(init + i) : safe;
-  }
-  __device__ __forceinline__ void meta_from(uint64_t i, const uint32_t (&x)[4], uint64_t& o, uint32_t& Llo,
-                                            uint32_t& s) const {
+  // buffer i's offset from base_addr(), length's low word and ~init, wave-uniform (scalar loads)
+  __device__ __forceinline__ void meta_s(uint64_t i, uint64_t& o, uint32_t& Llo, uint32_t& s) const {
     o = i * stride;
     Llo = (uint32_t)len;
-    s = ~(init ? x[3] : init_all);
+    s = ~(init ? ldc(init, i) : init_all);
   }
   __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   template <bool F = false>
@@ -454,15 +448,10 @@ struct VarGeom {
   __device__ __forceinline__ uint32_t lengths_lo(uint64_t i) const {  // (little-endian low word)
     return reinterpret_cast<const uint32_t*>(lengths)[2 * i];
   }
-  __device__ __forceinline__ uintptr_t meta_addr(uint64_t i, uint32_t f, uintptr_t safe) const {
-    return f < 2u ? (uintptr_t)(offsets + i) + 4u * f
-                  : (f == 2u ? (uintptr_t)(lengths + i) : (init ? (uintptr_t)(init + i) : safe));
-  }
-  __device__ __forceinline__ void meta_from(uint64_t, const uint32_t (&x)[4], uint64_t& o, uint32_t& Llo,
-                                            uint32_t& s) const {
-    o = ((uint64_t)x[1] << 32) | x[0];
-    Llo = x[2];
-    s = ~(init ? x[3] : init_all);
+  __device__ __forceinline__ void meta_s(uint64_t i, uint64_t& o, uint32_t& Llo, uint32_t& s) const {
+    o = ldc(offsets, i);
+    Llo = ldc(reinterpret_cast<const uint32_t*>(lengths), 2 * i);
+    s = ~(init ? ldc(init, i) : init_all);
   }
   __device__ __forceinline__ uintptr_t base_addr() const { return (uintptr_t)base; }
   __device__ __forceinline__ void locate(uint64_t t, uint64_t& i, uint32_t& c) const {
@@ -1650,17 +1639,17 @@ struct SlotPass {
 // The drain of a sub-range's lists, two passes per step with interleaved
 // chains, every wave of the workgroup pulling slots from one LDS counter.
 // Slot k < nB is list B's k-th entry (a J == 2 buffer: its head and body);
-// later slots hold two list-A entries each.  Pipeline: a step pulls the
-// slot after the next one, builds the words of the slot in hand (waiting for
-// its loads), turns the next slot's metadata -- loaded a step earlier --
-// into positions, issues the metadata load of the pulled slot and the next
-// slot's chunk loads, then runs the chains.  Past the end a pass is a dummy
-// chunk in the table blob (loaded, not written; a slot of two dummies is not
-// run).  The metadata is the offset, the length's low word (list entries
-// have at most two chunks or are heads: h = ((L - 1) & 4095) + 1, J == 1
-// from the entry's kLOut), ~init and a kTInj body's hc: the fewer registers
-// the next slot's loads hold, the more LDS lookups of the chains the
-// compiler keeps in flight.
+// later slots hold two list-A entries each.  Pipeline: a step builds the
+// words of the slot in hand (waiting for its loads), turns the next slot's
+// metadata -- loaded a step earlier, before those chunk loads -- into
+// positions, pulls the slot after it and issues its metadata loads, issues
+// the next slot's chunk loads, then runs the chains.  Past the end a pass is
+// a dummy chunk in the table blob (loaded, not written; a slot of two
+// dummies is not run).  The metadata is the offset, the length's low word
+// (list entries have at most two chunks or are heads: h = ((L - 1) & 4095)
+// + 1, J == 1 from the entry's kLOut) and ~init: the fewer registers the
+// next slot's loads hold, the more LDS lookups of the chains the compiler
+// keeps in flight.
 template <class G>
 __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t* lds, const LaneBase& lb,
                                            uint64_t sub0, uint32_t* ctl, const uint16_t* list, bool shortm) {
@@ -1674,38 +1663,22 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
     if (lane == 0) v = atomicAdd(&ctl[1], 1u);
     return uniform_u32(v);
   };
-  // Slot k's entries (wave-uniform tags from the LDS lists) and their
-  // metadata: ONE vector load per slot, issued a step before the slot's
-  // positions are made -- lane 5q + f loads field f of entry q (f = 0..3:
-  // G::meta_addr; f = 4: hc[i] of a kTInj body), read out with v_readlane.
-  // (Scalar metadata loads -- an s_load in flight makes every LDS wait of
-  // the chains wait for it too, so they had to land, exposed, between the
-  // word build and the chains -- and a separate hc load: v 85.2-87.4 vs
-  // 85.6-88.6 us over two boxes, r, f and config 3 unchanged -- within the
-  // noise, profiles/r03_ablations; the layout-computed metadata of the
-  // ablation saved ~5 us, so the load's cost is not all latency).  The load
-  // must be issued before the chunk loads: between them and the chains the
-  // compiler serialised the two chains, v 88.6 -> 99-104 us.)
-  auto entries = [&](uint32_t k, uint32_t& t0, uint32_t& t1) {
+  // Slot k's entries and their metadata -- scalar loads into SGPRs: the
+  // metadata of the next slot holds no vector registers across the chains
+  // (with vector loads the scheduler ran out of registers and serialised the
+  // two chains' LDS lookups)
+  uint64_t mo0, mo1;
+  uint32_t mL0, mL1, ms0, ms1, mj0, mj1;
+  auto meta = [&](uint32_t k) {
     const bool isb = k < nB;
     const uint32_t a = 2u * (k - nB);
     const uint32_t e0 = uniform_u32(isb ? (uint32_t)list[kHeadSub - 1u - k] : (a < nA ? (uint32_t)list[a] : 0u));
     const uint32_t e1 = uniform_u32(isb || a + 1u >= nA ? 0u : (uint32_t)list[a + 1u]);
-    t0 = isb ? (e0 | kTOk | kTPair) : (a < nA ? e0 | kTOk : 0u);
-    t1 = isb ? t0 : (a + 1u < nA ? e1 | kTOk : 0u);
+    mj0 = isb ? (e0 | kTOk | kTPair) : (a < nA ? e0 | kTOk : 0u);
+    mj1 = isb ? mj0 : (a + 1u < nA ? e1 | kTOk : 0u);
+    g.meta_s(sub0 + (mj0 & 1023u), mo0, mL0, ms0);
+    g.meta_s(sub0 + (mj1 & 1023u), mo1, mL1, ms1);
   };
-  const uint32_t mq = lane >= 5 ? 1u : 0u, mf = (uint32_t)lane - 5u * mq;
-  auto meta_issue = [&](uint32_t t0, uint32_t t1) -> uint32_t {
-    const uint32_t t = mq ? t1 : t0;
-    uintptr_t a = safe;
-    if (lane < 10 && (t & kTOk)) {
-      const uint64_t i = sub0 + (t & 1023u);
-      const bool inj = shortm && !(t & (kTPair | kLOut));  // a two-chunk buffer's body (kTInj, see pos)
-      a = mf < 4u ? g.meta_addr(i, mf, safe) : (inj ? (uintptr_t)(ka.hc + i) : safe);
-    }
-    return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)a);
-  };
-  auto rl = [](uint32_t v, uint32_t l) -> uint32_t { return lane_u32(v, l); };
   // positions of one entry; for a PAIR slot the first pass is the head, the
   // second the body
   auto pos = [&](uint64_t o, uint32_t L, uint32_t s, uint32_t tag, bool second, SlotPass& q) {
@@ -1738,32 +1711,21 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
       q.tag |= kTHc;
     }
   };
-  // slot (t0, t1)'s positions and hc registers from its metadata load v
-  auto take = [&](uint32_t v, uint32_t t0, uint32_t t1, SlotPass& A, SlotPass& B, uint32_t& xA, uint32_t& xB) {
-    const uint32_t x0[4] = {rl(v, 0), rl(v, 1), rl(v, 2), rl(v, 3)};
-    const uint32_t x1[4] = {rl(v, 5), rl(v, 6), rl(v, 7), rl(v, 8)};
-    uint64_t o0, o1;
-    uint32_t L0, L1, s0, s1;
-    g.meta_from(sub0 + (t0 & 1023u), x0, o0, L0, s0);
-    g.meta_from(sub0 + (t1 & 1023u), x1, o1, L1, s1);
-    pos(o0, L0, s0, t0, false, A);
-    pos(o1, L1, s1, t1, true, B);
-    xA = rl(v, 4);
-    xB = rl(v, 9);
+  auto aux_load = [&](const SlotPass& q) -> uint32_t {  // hc[i] of a kTInj pass (bypassing L1)
+    const uintptr_t a = (q.tag & kTInj) ? (uintptr_t)(ka.hc + sub0 + (q.tag & 1023u)) : safe;
+    return __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t*)a);
   };
   SlotPass A, B;
-  uint32_t t0, t1, xA, xB;
-  entries(pull(), t0, t1);
-  take(meta_issue(t0, t1), t0, t1, A, B, xA, xB);
+  meta(pull());
+  pos(mo0, mL0, ms0, mj0, false, A);
+  pos(mo1, mL1, ms1, mj1, true, B);
   Chunk cA, cB;
   load_general(A.ce, true, A.ps, lane, cA);
   load_general(B.ce, true, B.ps, lane, cB);
-  entries(pull(), t0, t1);
-  uint32_t mv = meta_issue(t0, t1);  // the next slot's metadata, behind its chunk loads
+  uint32_t xA = aux_load(A), xB = aux_load(B);
   while (true) {
     if (!(A.tag & kTOk)) break;  // (a slot wholly past the end: its loads just drain)
-    uint32_t u0, u1;
-    entries(pull(), u0, u1);  // the slot after the next (lands while this slot's words are built)
+    meta(pull());  // the next slot's (lands while this slot's words are built)
     uint32_t w[2][16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[0][q] = cA.d[q];
@@ -1784,12 +1746,12 @@ __device__ __forceinline__ void drain_list(const G& g, const KArgs& ka, uint8_t*
     // mixed batch whose body kernel re-runs this tile's two-chunk bodies
     const uint32_t hcA = iA ^ A.sx, hcB = iB ^ B.sx;
     const uint32_t uA = A.tag, uB = B.tag;
-    take(mv, t0, t1, A, B, xA, xB);  // the next slot (its metadata loaded a step ago)
-    mv = meta_issue(u0, u1);  // the slot after it
-    t0 = u0;
-    t1 = u1;
+    pos(mo0, mL0, ms0, mj0, false, A);
+    pos(mo1, mL1, ms1, mj1, true, B);
     load_general(A.ce, true, A.ps, lane, cA);
     load_general(B.ce, true, B.ps, lane, cB);
+    xA = aux_load(A);
+    xB = aux_load(B);
     // (The scheduler sinks the second pass's loads into the chains below to
     // keep the two chains' lookups interleaved; forcing every load ahead of
     // the chains -- an asm memory barrier -- serialised the chains and

@@ -1,0 +1,66 @@
+"""Per-workload PMC summary in the form of profiles/r03_pmc_summary.json from
+tools/pmc.sh output directories (one per workload).
+    python tools/pmc_workloads.py OUT.json name=DIR:ALG_BYTES:kernel1,kernel2 ...
+Every counter is the mean per dispatch over the workload's timed launches,
+scaled by launched waves (Grid_Size / 64) / SQ_WAVES (the share of SQ
+instances the counters sample); HBM read = FETCH_SIZE kB x 2 (gfx950 half
+count on 16-B/lane streams) x 1024, write = WRITE_SIZE kB x 1024
+(/opt/skills/guides/MI355X_MICROARCH.md)."""
+import csv, glob, json, os, sys
+from collections import defaultdict
+
+CFG2_VALU_PER_KB = 50.45  # profiles/r03_pmc_summary.json, config 2
+
+
+def kernel_counters(d, pat):
+    vals = defaultdict(lambda: defaultdict(float))
+    waves = {}
+    for f in sorted(glob.glob(os.path.join(d, "*counter_collection.csv"))):
+        for row in csv.DictReader(open(f)):
+            if pat not in row["Kernel_Name"]:
+                continue
+            key = (os.path.basename(f), row["Dispatch_Id"])
+            vals[row["Counter_Name"]][key] += float(row["Counter_Value"])
+            waves[key] = int(row["Grid_Size"]) // 64
+    out = {}
+    sq = vals.get("SQ_WAVES", {})
+    for c, per in vals.items():
+        acc = []
+        for key, v in per.items():
+            same_pass = [k for k in sq if k[0] == key[0]]
+            s = sum(sq[k] for k in same_pass) / max(1, len(same_pass)) if same_pass else 0.0
+            scale = (waves[key] / s) if (s and c != "SQ_WAVES") else 1.0
+            acc.append(v * scale)
+        out[c] = sum(acc) / len(acc)
+    return out
+
+
+res = {"source": "tools/pmc.sh passes, summarised by tools/pmc_workloads.py", "workloads": {}}
+for spec in sys.argv[2:]:
+    name, rest = spec.split("=", 1)
+    d, alg, kernels = rest.split(":")
+    alg = float(alg)
+    w = {"alg_bytes": alg, "kernels": {}}
+    tot = defaultdict(float)
+    for k in kernels.split(","):
+        c = kernel_counters(d, k)
+        rec = {x: round(c[x]) for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT",
+                                        "SQ_LDS_IDX_ACTIVE") if x in c}
+        if "FETCH_SIZE" in c:
+            rec["hbm_read_bytes"] = round(c["FETCH_SIZE"] * 2 * 1024)
+        if "WRITE_SIZE" in c:
+            rec["hbm_write_bytes"] = round(c["WRITE_SIZE"] * 1024)
+        w["kernels"][k] = rec
+        for x, v in rec.items():
+            tot[x] += v
+    kb = alg / 1024.0  # per KiB, as profiles/r03_pmc_summary.json
+    w["valu_per_kB"] = round(tot["SQ_INSTS_VALU"] / kb, 2)
+    w["salu_per_kB"] = round(tot["SQ_INSTS_SALU"] / kb, 2)
+    if tot["SQ_LDS_IDX_ACTIVE"]:
+        w["lds_bank_conflict_share"] = round(tot["SQ_LDS_BANK_CONFLICT"] / tot["SQ_LDS_IDX_ACTIVE"], 4)
+    if "hbm_read_bytes" in tot:
+        w["traffic_over_alg"] = round((tot["hbm_read_bytes"] + tot.get("hbm_write_bytes", 0)) / alg, 4)
+    w["valu_per_byte_vs_cfg2"] = round(w["valu_per_kB"] / CFG2_VALU_PER_KB, 3)
+    res["workloads"][name] = w
+json.dump(res, open(sys.argv[1], "w"), indent=1)
+print(json.dumps(res, indent=1))

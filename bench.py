@@ -89,34 +89,78 @@ def physical_cores() -> tuple:
     return len(cores), len(cpus)
 
 
-def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int) -> dict:
+def cgroup_cpu_max() -> str | None:
+    """The cgroup v2 CPU quota of this process ("max 100000" = none)."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = f.read().strip().split("\n")[0].split("::", 1)[-1]
+        for path in (f"/sys/fs/cgroup{rel}/cpu.max", "/sys/fs/cgroup/cpu.max"):
+            if os.path.exists(path):
+                with open(path) as f:
+                    return f.read().strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int, reps: int = 5) -> dict:
     """The reference's own util/crc32c.cc + port/port_posix_sse.cc (oracle/_ref;
     the clean-room port if absent) on this host: every physical core, and one
-    thread.  Each thread makes `reps` passes over its contiguous share of the
-    first n blocks inside ONE call (thread start-up paid once), reps sized
-    from a calibration call to ~`seconds`."""
+    thread.  Each leg is `reps` timed repetitions (median reported, BASELINE.md);
+    one repetition = `passes` passes over each thread's contiguous share of the
+    first n blocks inside ONE call (thread start-up paid once), sized from a
+    calibration call to ~seconds/reps.  Around every repetition the process's
+    CPU seconds (os.times, all threads) are read: CPU-seconds / wall = the
+    parallelism that actually ran, reported as `cores` -- a cgroup quota or a
+    busy host shows there, not in the thread count.  Plus the drop-in's own
+    single-buffer path (`single_buffer`): db/db_bench.cc:729-746's crc32c loop
+    (Value() of one 4 KiB buffer until 500 MB) through the reference's Value
+    and through nvl_crc32c_value on one core."""
     import oracle
     kind = "reference" if oracle.ref_available("sse") else "port"
     impl = oracle.ref("sse") if kind == "reference" else oracle.port()
 
-    def run(nblk, th, reps):
-        return impl.fixed_mt(host, BLOCK, BLOCK, nblk, th, reps=reps)
+    def run(nblk, th, passes):
+        return impl.fixed_mt(host, BLOCK, BLOCK, nblk, th, reps=passes)
 
-    def timed(nblk, th):
+    def leg(nblk, th):
         t0 = time.perf_counter()
-        run(nblk, th, 1)  # calibration (also warms the pages)
+        r = run(nblk, th, 1)  # calibration (also warms the pages)
         one = max(time.perf_counter() - t0, 1e-4)
-        reps = max(1, int(seconds / one))
-        t0 = time.perf_counter()
-        r = run(nblk, th, reps)
-        el = time.perf_counter() - t0
-        return r, reps * nblk * BLOCK / el / 2**30, reps, el
+        passes = max(1, int(seconds / reps / one))
+        rates, par = [], []
+        for _ in range(reps):
+            c0, t0 = os.times(), time.perf_counter()
+            run(nblk, th, passes)
+            el = time.perf_counter() - t0
+            c1 = os.times()
+            rates.append(passes * nblk * BLOCK / el / 2**30)
+            par.append(((c1.user - c0.user) + (c1.system - c0.system)) / el)
+        return r, float(np.median(rates)), float(np.median(par)), passes, rates
 
     phys, logical = physical_cores()
     th = threads if threads > 0 else phys
-    r_all, gibs_all, reps_all, el_all = timed(n, th)
+    r_all, gibs_all, par_all, passes_all, rates_all = leg(n, th)
     n1 = min(n, 20000)
-    r_one, gibs_one, reps_one, el_one = timed(n1, 1)
+    _, gibs_one, par_one, passes_one, rates_one = leg(n1, 1)
+    single = None
+    if kind == "reference" and hasattr(impl.lib, "ref_dbbench_crc32c"):
+        import ctypes
+        from nvlevelz_amd import _lib
+        fn = ctypes.cast(_lib.lib.nvl_crc32c_value, ctypes.c_void_p).value
+        ref_r, nvl_r = [], []
+        for _ in range(reps):
+            g, c_ref = impl.dbbench_crc32c(None)
+            ref_r.append(g)
+            g, c_nvl = impl.dbbench_crc32c(fn)
+            nvl_r.append(g)
+        single = {"reference": round(float(np.median(ref_r)), 3), "nvl_crc32c_value": round(float(np.median(nvl_r)), 3),
+                  "unit": "GiB/s", "cores": 1, "ratio": round(float(np.median(nvl_r) / np.median(ref_r)), 3),
+                  "same_crc": c_ref == c_nvl,
+                  "what": "db/db_bench.cc:729-746 crc32c loop: Value() of one 4 KiB buffer until 500 MB, one "
+                          "thread; the reference's leveldb::crc32c::Value (oracle/_ref, SSE4.2 crc32q) against "
+                          "the drop-in's nvl_crc32c_value (include/nvl_crc32c.h; integration/"
+                          "leveldb_util_crc32c.cc forwards Extend to it), median of 5 alternating runs"}
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -127,13 +171,20 @@ def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int) -> dict
     except OSError:
         pass
     return {
-        "value": round(gibs_all, 3), "unit": "GiB/s", "cores": th, "kind": kind,
-        "sample": f"{reps_all} passes over the first {n} x 4 KiB blocks of this rank's batch "
-                  f"({el_all:.1f} s, {th} threads = every physical core of the {logical} CPUs in this "
-                  f"process's affinity set, contiguous share per thread), "
-                  f"leveldb::crc32c::Value via port::AcceleratedCRC32C (SSE4.2)",
+        "value": round(gibs_all, 3), "unit": "GiB/s", "cores": int(round(par_all)), "kind": kind,
+        "threads": th, "effective_parallelism": round(par_all, 2),
+        "per_thread_gibs": round(gibs_all / max(par_all, 1e-9), 3),
+        "sample": f"median of {reps} repetitions x {passes_all} passes over the first {n} x 4 KiB blocks of this "
+                  f"rank's batch ({th} threads = every physical core of the {logical} CPUs in this process's "
+                  f"affinity set, contiguous share per thread; cores = CPU-seconds / wall of the run = "
+                  f"{par_all:.1f}), leveldb::crc32c::Value via port::AcceleratedCRC32C (SSE4.2)",
+        "repetitions_gibs": [round(x, 2) for x in rates_all],
+        "cgroup_cpu_max": cgroup_cpu_max(),
         "single_thread": {"value": round(gibs_one, 3), "unit": "GiB/s", "cores": 1,
-                          "sample": f"{reps_one} passes over {n1} blocks ({el_one:.1f} s)"},
+                          "effective_parallelism": round(par_one, 2),
+                          "sample": f"median of {reps} x {passes_one} passes over {n1} blocks",
+                          "repetitions_gibs": [round(x, 2) for x in rates_one]},
+        "single_buffer": single,
         "host_cpu": model, "host_nproc": os.cpu_count(), "physical_cores": phys, "affinity_cpus": logical,
         "_check": r_all,
     }

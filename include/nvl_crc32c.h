@@ -142,6 +142,31 @@ NVL_API int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, cons
 /* Workspace bytes nvl_crc32c_batch_dev needs for n buffers. */
 NVL_API size_t nvl_crc32c_batch_workspace_bytes(uint64_t n);
 
+/* Region batch: buffer i is lengths[i] bytes at region + offsets[i] (device
+ * memory; offsets relative to `region`), for buffers that lie inside ONE
+ * region [region, region + region_len) sorted by offset and non-overlapping
+ * -- an SSTable image's blocks in file order (table/format.cc:90-92 for each),
+ * a log image's records, a packed batch.  The region is checksummed in its
+ * own page-aligned 4 KiB chunks at the fixed-stride path's rate whatever the
+ * buffers' lengths and alignment, and each out[i] is derived from the chunk
+ * values (Mask()ed with NVL_CRC32C_FLAG_MASK).  A batch that breaks the
+ * layout (unsorted, overlapping, outside the region) still gets correct
+ * results, by a slow serial path: use nvl_crc32c_batch_dev for such batches.
+ * Gaps between buffers cost their bytes (the whole region is read). */
+NVL_API int nvl_crc32c_region_dev(const void* region, uint64_t region_len, const uint64_t* offsets,
+                                  const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
+                                  uint64_t n, uint32_t flags, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Measurement form (as nvl_crc32c_fixed_dev_timed): the first kernel records
+ * start_event, the last stop_event. */
+NVL_API int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len, const uint64_t* offsets,
+                                        const uint64_t* lengths, const uint32_t* init, uint32_t init_all,
+                                        uint32_t* out, uint64_t n, uint32_t flags, void* workspace,
+                                        size_t workspace_bytes, void* stream, void* start_event, void* stop_event);
+
+/* Workspace bytes nvl_crc32c_region_dev needs (4 B per 4 KiB of region + 8 B per buffer). */
+NVL_API size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n);
+
 /* ---- batched, host-resident (end-to-end path) ---------------------------- */
 
 /* Host buffers in, host results out, synchronous: stages the buffers through

@@ -53,6 +53,10 @@ SIGNATURES = {
     "nvl_crc32c_fixed_host": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _u32]),
     "nvl_crc32c_fill_splitmix": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
     "nvl_crc32c_batch_region_host": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32]),
+    "nvl_crc32c_region_dev": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32, _vp, _sz, _vp]),
+    "nvl_crc32c_region_dev_timed": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32, _vp, _sz, _vp, _vp,
+                                           _vp]),
+    "nvl_crc32c_region_workspace_bytes": (_sz, [_u64, _u64]),
     # include/nvl_framing.h
     "nvl_sstable_seal_trailers": (_int, [_vp, _u64, _vp, _sz, _u32]),
     "nvl_sstable_verify_blocks": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _u32]),

@@ -244,6 +244,47 @@ def extend_batch(buf, offsets, lengths, init=0, *, mask: bool = False, out=None,
     return out
 
 
+def region_workspace_bytes(region_len: int, n: int) -> int:
+    return int(lib.nvl_crc32c_region_workspace_bytes(region_len, n))
+
+
+def extend_region(buf, offsets, lengths, init=0, *, mask: bool = False, out=None, workspace=None):
+    """out[i] = Extend(init_i, buf[offsets[i] : offsets[i] + lengths[i]]) for
+    buffers inside ``buf`` sorted by offset and non-overlapping (an SSTable
+    image's blocks, a packed batch): nvl_crc32c_region_dev, which reads the
+    whole of ``buf`` in page-aligned 4 KiB chunks.  Other layouts are correct
+    but slow there; use extend_batch for them.  Asynchronous."""
+    torch = _torch()
+    _require_dev(buf, "buf", (torch.uint8, torch.int8))
+    _require_dev(offsets, "offsets", (torch.int64, torch.uint64), buf.device)
+    _require_dev(lengths, "lengths", (torch.int64, torch.uint64), buf.device)
+    n = offsets.numel()
+    if lengths.numel() != n:
+        raise ValueError("offsets and lengths differ in size")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=buf.device)
+    _require_dev(out, "out", (torch.int32, torch.uint32), buf.device)
+    if out.numel() < n:
+        raise ValueError("out too small")
+    init_ptr, init_all = None, 0
+    if isinstance(init, int):
+        init_all = init & 0xFFFFFFFF
+    else:
+        _require_dev(init, "init", (torch.int32, torch.uint32), buf.device)
+        if init.numel() < n:
+            raise ValueError("init too small")
+        init_ptr = init.data_ptr()
+    ws_ptr, ws_bytes = None, 0
+    if workspace is not None:
+        _require_dev(workspace, "workspace", None, buf.device)
+        ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    rc = lib.nvl_crc32c_region_dev(buf.data_ptr(), buf.numel(), offsets.data_ptr(), lengths.data_ptr(), init_ptr,
+                                   init_all, out.data_ptr(), n, FLAG_MASK if mask else 0, ws_ptr, ws_bytes,
+                                   _stream_handle(buf))
+    check(rc, "nvl_crc32c_region_dev")
+    return out
+
+
 def extend_batch_host(buffers: Sequence[BytesLike], init: Union[int, Sequence[int]] = 0, *,
                       mask: bool = False) -> np.ndarray:
     """Host buffers in, u32 CRCs out (synchronous; pinned staging + GPU)."""

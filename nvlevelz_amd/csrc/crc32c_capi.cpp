@@ -35,6 +35,18 @@ void build_device_tables(uint32_t* w) {
   build_shift_op(pw.x2n, 4096, op);
   memcpy(w + 7168, op, sizeof(op));
   memcpy(w + 8192, pw.x2n, sizeof(pw.x2n));
+  // Powers of x^8 and of its inverse for the region fold.  Multiplying by x
+  // in the reflected form is v >> 1 (^ P when bit 0 = x^31 overflows); its
+  // inverse: bit 31 (x^0) set means P was added, so v = ((v ^ P) << 1) | 1.
+  uint32_t p = kOne, q = kOne;
+  for (uint32_t d = 0; d <= 4096; ++d) {
+    w[kTabXp8 + d] = p;
+    if (d < 4096) w[kTabXm8 + d] = q;
+    for (int b = 0; b < 8; ++b) {
+      p = (p >> 1) ^ ((p & 1u) ? kPolyReflected : 0u);
+      q = (q & kOne) ? (((q ^ kPolyReflected) << 1) | 1u) : (q << 1);
+    }
+  }
 }
 
 namespace {
@@ -265,6 +277,39 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
                    flags, recs, hc, long_bufs, small);
   if (own) (void)hipFreeAsync(ws, st);
   return hip_rc(e);
+}
+
+// Region batch: page-aligned chunk pass + per-buffer fold (launch_region).
+// Needs the stream's counter block; without one (more than
+// kMaxCounterStreams streams) the batch runs through do_batch instead.
+int do_region(DeviceState* s, const void* region, uint64_t region_len, const uint64_t* offsets,
+              const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
+              uint32_t flags, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t ev_start = nullptr,
+              hipEvent_t ev_stop = nullptr) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!offsets || !lengths || !out || !region) return NVL_CRC32C_EINVAL;
+  if (n >= (1ull << 31) - 2 || region_len > (1ull << 50)) return NVL_CRC32C_EINVAL;
+  LaunchCtx lc{st, s->num_cu, s->tables, counters_for(s, st), ev_start, ev_stop};
+  if (!lc.counter) return do_batch(s, region, offsets, lengths, init, init_all, out, n, flags, nullptr, 0, st);
+  const size_t need = region_ws_bytes(region_len, n);
+  bool own = false;
+  if (!ws) {
+    if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
+    own = true;
+  } else if (ws_bytes < need) {
+    return NVL_CRC32C_ENOSPC;
+  }
+  hipError_t e = launch_region(lc, static_cast<const uint8_t*>(region), region_len, offsets, lengths, init, init_all,
+                               out, n, flags, ws);
+  if (own) (void)hipFreeAsync(ws, st);
+  return hip_rc(e);
+}
+
+// Sorted by offset and non-overlapping (what the region pass is fast for).
+bool region_sorted(const uint64_t* offsets, const uint64_t* lengths, uint64_t n) {
+  for (uint64_t i = 1; i < n; ++i)
+    if (offsets[i] < offsets[i - 1] + lengths[i - 1]) return false;
+  return true;
 }
 
 // Known-answer probe on the GPU: "TestCRCBuffer" -> 0xdcbc59fa at every
@@ -652,6 +697,34 @@ int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64
                   static_cast<hipStream_t>(stream));
 }
 
+size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n) { return region_ws_bytes(region_len, n); }
+
+int nvl_crc32c_region_dev(const void* region, uint64_t region_len, const uint64_t* offsets, const uint64_t* lengths,
+                          const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  int dev = -1;
+  int rc = stream_device(static_cast<hipStream_t>(stream), &dev);
+  if (rc != NVL_CRC32C_OK) return rc;
+  DeviceState* s = state_for(dev, &rc);
+  if (!s) return rc;
+  return do_region(s, region, region_len, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
+                   static_cast<hipStream_t>(stream));
+}
+
+int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len, const uint64_t* offsets,
+                                const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
+                                uint64_t n, uint32_t flags, void* workspace, size_t workspace_bytes, void* stream,
+                                void* start_event, void* stop_event) {
+  int dev = -1;
+  int rc = stream_device(static_cast<hipStream_t>(stream), &dev);
+  if (rc != NVL_CRC32C_OK) return rc;
+  DeviceState* s = state_for(dev, &rc);
+  if (!s) return rc;
+  return do_region(s, region, region_len, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
+                   static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
+                   static_cast<hipEvent_t>(stop_event));
+}
+
 int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, const uint32_t* init,
                           uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags) {
   if (n == 0) return NVL_CRC32C_OK;
@@ -760,7 +833,9 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
   size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
-  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
+  const bool sorted = region_sorted(offsets, lengths, n);
+  const size_t ws = sorted ? region_ws_bytes(wbytes, n)
+                           : batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
   const size_t dbytes = align_up(total, 256) + align_up(n * 4, 256) + ws + 256;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
@@ -778,7 +853,10 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     hini[i] = init ? init[i] : init_all;
   }
   if (e == hipSuccess) e = hipMemcpyAsync(d + meta_off, hst + meta_off, total - meta_off, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess)
+  if (e == hipSuccess && sorted)
+    rc = do_region(s, d, wbytes, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
+                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);
+  else if (e == hipSuccess)
     rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
   else

@@ -17,7 +17,10 @@ namespace nvl {
 //   [1024,  7168)  comb[6][4][256]    shift by 64*2^k bytes, byte-sliced
 //   [7168,  8192)  sh4096[4][256]     shift by 4096 bytes, byte-sliced
 //   [8192,  8256)  x2n[64]            x^(2^k) mod P
-constexpr uint32_t kTableWords = 8256;
+//   [8256, 12353)  xp8[4097]          x^(8d) mod P, d = 0..4096        (region fold)
+//   [12353,16449)  xm8[4096]          x^(-8d) mod P, d = 0..4095       (region fold)
+constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + 4097;
+constexpr uint32_t kTableWords = kTabXm8 + 4096;
 
 // A portion of one buffer processed inside one work unit (fix-up input).
 struct Rec {
@@ -84,6 +87,16 @@ hipError_t launch_var_fused(const LaunchCtx& lc, const uint8_t* base, const uint
 // The head kernel finishes every buffer of an n-buffer batch whose lengths
 // are all <= max_len: two chunks at most, one sub-range per tile.
 bool var_heads_only(int num_cu, uint64_t n, uint64_t max_len);
+
+// Region batch (nvl_crc32c_region_dev): n buffers inside [region, region +
+// region_len), checksummed over the region's page-aligned 4 KiB chunks and
+// folded per buffer.  ws: region_ws_bytes(region_len, n).  counter: the
+// stream's counter block (words kRegionFlag / kRegionDone).
+size_t region_ws_bytes(uint64_t region_len, uint64_t n);
+hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
+                         const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
+                         uint32_t flags, void* ws);
+constexpr uint32_t kRegionFlag = 16, kRegionDone = 17;  // counter-block words (the fused kernel uses word 0)
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

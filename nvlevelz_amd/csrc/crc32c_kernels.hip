@@ -2700,6 +2700,395 @@ __global__ void crc32c_trailer_verdicts(const uint8_t* __restrict__ f, const uin
                                              : (t[0] > 1u ? 3u /* NVL_BLOCK_BAD_TYPE */ : 0u);
 }
 
+// ---------------------------------------------------------------------------
+// Region batches (nvl_crc32c_region_dev): the n buffers lie inside ONE region
+// (an SSTable image's blocks, a log image's records, config 3's packed
+// buffers), sorted by offset and non-overlapping.  Instead of one pass per
+// buffer-aligned chunk -- a 3.4..4.1 KiB block costs a whole 4 KiB pass and
+// its head a second -- the region is streamed in ITS OWN page-aligned 4 KiB
+// chunks at scheduler A's rate, and every buffer is derived from chunk-level
+// values (model: tests/kernel_model.py region_batch):
+//   chunk c = [4096c, 4096c + 4096) from the grid origin O = region & ~4095,
+//   raws[c] = raw(0, chunk c);
+//   for a buffer boundary ("event") at in-chunk offset p (not 0), lane L = p/64
+//     holds it: Qe = the butterfly over the lanes below L with the others
+//     zeroed = raw(0, chunk bytes [0, 64L)) shifted to the chunk end;
+//   the fold kernel re-reads the piece bytes [64L, p) (R = their raw) and
+//     combines: Ze(p) = Qe ^ shift(R, 4096 - p) is the chunk prefix before p
+//     at the chunk end, so a buffer [s, e) is
+//       acc = raws[c0] ^ Ze(s) (^ ~init injected at s), shift4096 ^ raws[c]
+//       over the chunks in between, then unshifted from the end of e's chunk:
+//       raw = (acc' ^ Qe(e)) * x^(-8(4096 - p_e)) ^ R(e).
+// The buffers are found per work unit from a 64-buffer window of the
+// metadata (lane j = buffer cursor + j) whose cursor the previous unit's
+// window gives, so there is no plan launch; a 64-ary search places each
+// wave's first cursor.  Events need the ends to be non-decreasing: the waves
+// check the batch (sorted, non-overlapping, inside the region) and any
+// violation sets a flag with which the fold kernel checksums every buffer
+// serially instead (correct, slow).
+constexpr uint32_t kRegionDirect = 64;  // shorter buffers: checksummed whole by the fold kernel
+
+struct RegionGeom {
+  const uint8_t* grid;  // O: chunk c at grid + 4096c
+  uint64_t nc;          // chunks
+  uint64_t rel0;        // region - O
+  uint64_t region_len;
+  const uint64_t* offsets;  // from the region start
+  const uint64_t* lengths;
+  uint64_t n;
+  uint32_t* raws;  // [nc]
+  uint32_t* qs;    // [n] Qe of buffer i's start event
+  uint32_t* qe;    // [n] Qe of its end event
+  uint32_t* ctr;   // the stream's counter block
+};
+
+typedef const __attribute__((address_space(1))) uint64_t* g64_ptr;
+__device__ __forceinline__ uint64_t ldg64(const uint64_t* p, uint64_t i) { return ((g64_ptr)p)[i]; }
+
+// One lane's buffer of a 64-buffer metadata window.
+struct WinRaw {
+  uint64_t off, len;
+};
+struct Win {
+  uint64_t s, e;  // grid-relative [s, e)
+  bool valid;     // cursor + lane < n
+  bool big;       // valid and at least kRegionDirect bytes (has events)
+};
+
+// Loads of the window at `cur` (the index is clamped so that the loads are
+// unconditional: a load behind a branch makes the compiler wait for it).
+__device__ __forceinline__ WinRaw load_win(const RegionGeom& g, uint64_t cur, int lane) {
+  const uint64_t b = min(cur + (uint64_t)lane, g.n - 1u);
+  return WinRaw{ldg64(g.offsets, b), ldg64(g.lengths, b)};
+}
+__device__ __forceinline__ Win make_win(const RegionGeom& g, const WinRaw& r, uint64_t cur, int lane) {
+  Win w;
+  w.valid = cur + (uint64_t)lane < g.n;
+  w.s = g.rel0 + r.off;
+  w.e = w.s + r.len;
+  w.big = w.valid && r.len >= kRegionDirect;
+  return w;
+}
+
+// First buffer b with e_b > A (n when none), for non-decreasing ends: a
+// 64-ary search, one wave-wide load per level.
+__device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane) {
+  uint64_t lo = 0, hi = g.n;  // every b < lo has e_b <= A; the answer is <= hi
+  while (hi - lo > 64u) {
+    const uint64_t step = (hi - lo + 63u) / 64u;
+    const uint64_t b = min(lo + (uint64_t)lane * step, hi - 1u);
+    const uint64_t e = g.rel0 + ldg64(g.offsets, b) + ldg64(g.lengths, b);
+    const uint64_t m = __ballot(e > A);
+    if (m == 0) {
+      lo = min(lo + 63u * step, hi - 1u) + 1u;
+    } else {
+      const uint32_t k = (uint32_t)__builtin_ctzll(m);
+      const uint64_t pk = min(lo + (uint64_t)k * step, hi - 1u);
+      lo = k ? lo + (uint64_t)(k - 1u) * step + 1u : lo;
+      hi = pk;
+    }
+  }
+  const uint64_t b = lo + (uint64_t)lane;
+  const uint64_t bc = min(b, g.n - 1u);
+  const uint64_t e = g.rel0 + ldg64(g.offsets, bc) + ldg64(g.lengths, bc);
+  const uint64_t m = __ballot(b < hi && e > A);
+  return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
+}
+
+// Chains and butterflies of U chunks, keeping each lane's piece raw (the
+// input of the events' masked butterflies).
+template <int U>
+__device__ __forceinline__ void chains_keep(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
+                                            int lane, uint32_t (&lr)[U], uint32_t (&raw)[U]) {
+  uint32_t crc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = w[u][0];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) lr[u] = crc[u];
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, 0, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, 1, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, 2, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, 3, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, 4, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, 5, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) raw[u] = crc[u];
+}
+
+// Qe(L): the butterfly over the lanes below L, the others zeroed.
+__device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr, uint32_t L, int lane) {
+  uint32_t g = (uint32_t)lane < L ? lr : 0u;
+  g = fold_level<0, 0, false>(lds, g, lane);
+  g = fold_level<1, 1, false>(lds, g, lane);
+  g = fold_level<2, 2, false>(lds, g, lane);
+  g = fold_level<3, 3, false>(lds, g, lane);
+  g = fold_level<4, 4, false>(lds, g, lane);
+  g = fold_level<5, 5, false>(lds, g, lane);
+  return uniform_u32(g);
+}
+
+// The events of chunks [ca, ca + cu) (lr[k]: chunk ca + k's lane raws): Qe
+// for every start and end of a big buffer strictly inside a chunk, in
+// position order (consecutive events on one lane of one chunk share Qe).
+// `w` is the window at `cur`; further windows are loaded while the last
+// buffer of the current one still starts before the unit's end.
+template <int U>
+__device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t* lds, Win w, uint64_t cur,
+                                              uint64_t ca, uint32_t cu, const uint32_t (&lr)[U], int lane) {
+  const uint64_t A = ca * kChunk, B = (ca + cu) * kChunk;
+  uint32_t pk = ~0u, pL = ~0u, pq = 0;
+  for (;;) {
+    const bool sv = w.big && (w.s & (kChunk - 1u)) != 0u && w.s >= A && w.s < B;
+    const bool ev = w.big && (w.e & (kChunk - 1u)) != 0u && w.e > A && w.e < B;
+    const uint64_t ms = __ballot(sv), me = __ballot(ev);
+    uint64_t all = ms | me;
+    while (all) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(all);
+      all &= all - 1u;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {  // start, then end
+        if (!(((t ? me : ms) >> j) & 1u)) continue;
+        const uint32_t pos = (uint32_t)(lane_u64(t ? w.e : w.s, j) - A);
+        const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6;
+        if (k != pk || L != pL) {
+          uint32_t v = lr[0];
+#pragma unroll
+          for (int q = 1; q < U; ++q) v = k == (uint32_t)q ? lr[q] : v;
+          pq = masked_fold(lds, v, L, lane);
+          pk = k;
+          pL = L;
+        }
+        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = pq;
+      }
+    }
+    if (cur + 64u >= g.n || lane_u64(w.s, 63) >= B) break;
+    cur += 64u;  // the unit's buffers run past the window (short buffers): the next one
+    w = make_win(g, load_win(g, cur, lane), cur, lane);
+  }
+}
+
+// Scheduler A over the region's chunks: the workgroup owns a contiguous
+// chunk range, its waves pull 2-chunk units from an LDS counter, the next
+// unit's chunks and metadata window are in flight while this one computes.
+template <int U>
+__device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
+  const uint64_t B0 = g.nc * blockIdx.x / gridDim.x;
+  const uint64_t B1 = g.nc * (blockIdx.x + 1) / gridDim.x;
+  const uint32_t cnt = (uint32_t)(B1 - B0);
+  const uint32_t nfull = cnt > kTail ? (cnt - kTail) / U : 0u;
+  const uint32_t nunits = nfull + (cnt - nfull * U);
+  auto first_of = [&](uint32_t u) -> uint64_t {
+    return u < nfull ? B0 + (uint64_t)u * U : B0 + (uint64_t)nfull * U + (u - nfull);
+  };
+  auto count_of = [&](uint32_t u) -> uint32_t { return u >= nunits ? 0u : (u < nfull ? (uint32_t)U : 1u); };
+  auto load_unit = [&](uint64_t ca, uint32_t cu, Chunk (&ch)[U]) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if ((uint32_t)k < cu) {
+        const uintptr_t cs = (uintptr_t)g.grid + (ca + (uint64_t)k) * kChunk;
+        const uint32_t lo = lane_load_off(lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u32x4 v = ld16(cs + 1024u * (uint32_t)j + lo);
+          ch[k].d[4 * j + 0] = v.x; ch[k].d[4 * j + 1] = v.y; ch[k].d[4 * j + 2] = v.z; ch[k].d[4 * j + 3] = v.w;
+        }
+      }
+    }
+  };
+
+  uint32_t u = wv;  // first unit pre-assigned: its loads overlap the search and the LDS fill
+  uint64_t ca = first_of(u);
+  uint32_t cu = count_of(u);
+  Chunk cur[U];
+  load_unit(ca, cu, cur);
+  uint64_t cursor = cu ? region_search(g, ca * kChunk, lane) : g.n;
+  WinRaw wr = load_win(g, cursor, lane);
+  fill_lds<kWavesPerWG>(lds, ka.tables);
+  __syncthreads();
+  const LaneBase lb = make_lane_base(lane);
+
+  while (u < nunits) {
+    const uint32_t un = pull_unit(lds, lane);
+    const Win w = make_win(g, wr, cursor, lane);
+    const uint64_t can = first_of(un);
+    const uint32_t cun = count_of(un);
+    uint64_t ncur = g.n;
+    if (cun) {  // the next unit's cursor: the first buffer of this window ending after its start
+      const uint64_t m = __ballot(w.valid && w.e > can * kChunk);
+      ncur = m ? cursor + (uint64_t)__builtin_ctzll(m) : min(cursor + 64u, g.n);
+    }
+    const WinRaw nwr = load_win(g, ncur, lane);
+    Chunk nxt[U];
+    load_unit(can, cun, nxt);
+
+    uint32_t lr[U], raw[U];
+    if (cu == (uint32_t)U) {
+      uint32_t wd[U][16];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
+        row_transpose(wd[k]);
+      }
+      chains_keep<U>(lds, lb, wd, lane, lr, raw);
+    } else {  // the range's single-chunk units
+      uint32_t wd[1][16], l1[1], r1[1];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wd[0][q] = cur[0].d[q];
+      row_transpose(wd[0]);
+      chains_keep<1>(lds, lb, wd, lane, l1, r1);
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        lr[k] = l1[0];
+        raw[k] = r1[0];
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
+    }
+    region_events<U>(g, lds, w, cursor, ca, cu, lr, lane);
+
+    u = un;
+    ca = can;
+    cu = cun;
+    cursor = ncur;
+    wr = nwr;
+#pragma unroll
+    for (int k = 0; k < U; ++k) cur[k] = nxt[k];
+  }
+
+  // The batch check, one slice per wave (after its units: the waves end
+  // apart anyway): sorted by offset, non-overlapping, inside the region.
+  const uint64_t per = (g.n + (uint64_t)gridDim.x * kWavesPerWG - 1u) / ((uint64_t)gridDim.x * kWavesPerWG);
+  const uint64_t i0 = min(g.n, ((uint64_t)blockIdx.x * kWavesPerWG + wv) * per), i1 = min(g.n, i0 + per);
+  bool bad = false;
+  for (uint64_t i = i0 + (uint64_t)lane; i < i1; i += 64u) {
+    const uint64_t o = ldg64(g.offsets, i), L = ldg64(g.lengths, i);
+    bad |= o > g.region_len || L > g.region_len - o;
+    if (i > 0) bad |= o < ldg64(g.offsets, i - 1) + ldg64(g.lengths, i - 1);
+  }
+  if (__ballot(bad) && lane == 0) g.ctr[kRegionFlag] = 1u;
+}
+
+__global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  run_region<NVL_FAST_U>(g, ka, lds);
+}
+
+// Per-buffer fold of a region batch (one thread per buffer).
+struct RegionFold {
+  const uint8_t* grid;
+  uint64_t rel0;
+  const uint64_t* offsets;
+  const uint64_t* lengths;
+  uint64_t n;
+  const uint32_t* init;
+  uint32_t init_all, flags;
+  const uint32_t* raws;
+  const uint32_t* qs;
+  const uint32_t* qe;
+  const uint32_t* tables;
+  uint32_t* out;
+  uint32_t* ctr;
+};
+
+__device__ __forceinline__ uint32_t fold_slice4(const uint32_t* t, uint32_t x) {
+  return t[768u + (x & 255u)] ^ t[512u + ((x >> 8) & 255u)] ^ t[256u + ((x >> 16) & 255u)] ^ t[x >> 24];
+}
+__device__ __forceinline__ uint32_t fold_step1(const uint32_t* t, uint32_t crc, uint32_t b) {
+  return t[(crc ^ b) & 255u] ^ (crc >> 8);
+}
+
+// raw(s, [p, p + L)) serially: bytes to a 4-byte boundary, STEP4 words, bytes.
+__device__ uint32_t serial_raw(const uint32_t* t, uint32_t crc, const uint8_t* p, uint64_t L) {
+  while (L && ((uintptr_t)p & 3u)) {
+    crc = fold_step1(t, crc, *p++);
+    --L;
+  }
+  for (; L >= 4; L -= 4, p += 4) crc = fold_slice4(t, crc ^ *reinterpret_cast<const uint32_t*>(p));
+  while (L--) crc = fold_step1(t, crc, *p++);
+  return crc;
+}
+
+// R(p) = raw(0, grid bytes [p & ~63, p)): a prefix of one 64-byte piece
+// (64-byte aligned: the grid origin is page-aligned).
+__device__ __forceinline__ uint32_t piece_prefix(const uint32_t* t, const uint8_t* grid, uint64_t p) {
+  const uint32_t o = (uint32_t)(p & 63u);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(grid + (p & ~(uint64_t)63));
+  uint32_t crc = 0;
+  for (uint32_t k = 0; k < (o >> 2); ++k) crc = fold_slice4(t, crc ^ w[k]);
+  if (o & 3u) {
+    const uint32_t x = w[o >> 2];
+    for (uint32_t b = 0; b < (o & 3u); ++b) crc = fold_step1(t, crc, (x >> (8u * b)) & 255u);
+  }
+  return crc;
+}
+
+__global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
+  __shared__ uint32_t sl[1024];  // slice4 t[k][b] (util/crc32c.cc table0_..table3_)
+  __shared__ uint32_t sh[1024];  // shift by 4096 bytes, byte-sliced
+  for (uint32_t t = threadIdx.x; t < 1024u; t += blockDim.x) {
+    sl[t] = a.tables[kGSlice + t];
+    sh[t] = a.tables[kGComb + 6u * 1024u + t];
+  }
+  const bool bad = ldc(a.ctr, kRegionFlag) != 0u;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.n) {
+    const uint64_t off = a.offsets[i], L = a.lengths[i];
+    const uint32_t ninit = ~(a.init ? a.init[i] : a.init_all);
+    const uint64_t s = a.rel0 + off;
+    uint32_t v;
+    if (bad || L < kRegionDirect) {
+      v = serial_raw(sl, ninit, a.grid + s, L);
+    } else {
+      const uint64_t e = s + L;
+      const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
+      const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));
+      uint32_t zs = gf_mul(a.tables[kTabXp8 + kChunk - os], (os ? piece_prefix(sl, a.grid, s) : 0u) ^ ninit);
+      if (os) zs ^= a.qs[i];
+      uint32_t acc = zs;
+      if (c0 != c1) {
+        acc ^= a.raws[c0];
+        for (uint64_t c = c0 + 1u; c < c1; ++c)
+          acc = sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^
+                sh[768u + (acc >> 24)] ^ a.raws[c];
+        acc = sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)];
+      }
+      if (oe == kChunk)
+        v = acc ^ a.raws[c1];
+      else
+        v = gf_mul(a.tables[kTabXm8 + kChunk - oe], acc ^ a.qe[i]) ^ piece_prefix(sl, a.grid, e);
+    }
+    a.out[i] = finish(~v, a.flags);
+  }
+  // The last workgroup re-zeroes the flag and the done count (every
+  // workgroup read the flag before its add).
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t d = __hip_atomic_fetch_add(a.ctr + kRegionDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1u) {
+      a.ctr[kRegionFlag] = 0u;
+      a.ctr[kRegionDone] = 0u;
+    }
+  }
+}
+
 // Synthetic stream: one thread per 8-byte word.
 __global__ void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t words_per_block, uint64_t nwords,
                                      uint64_t first_block, uint64_t block_step, uint64_t seed) {
@@ -2951,6 +3340,46 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, lc.stream);
+}
+
+// Region workspace: [raws: chunks u32][qs: n u32][qe: n u32] (chunks bounded
+// by region_len / 4096 + 2 whatever the region's alignment).
+static inline size_t align256(size_t v) { return (v + 255u) / 256u * 256u; }
+size_t region_ws_bytes(uint64_t region_len, uint64_t n) {
+  return align256((region_len / dev::kChunk + 2u) * 4u) + 2u * align256(n * 4u);
+}
+
+hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
+                         const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
+                         uint32_t flags, void* ws) {
+  if (n == 0) return hipSuccess;
+  if (!lc.counter) return hipErrorInvalidValue;
+  const uintptr_t O = (uintptr_t)region & ~(uintptr_t)(dev::kChunk - 1u);
+  const uint64_t rel0 = (uintptr_t)region - O;
+  const uint64_t nc = (rel0 + region_len + dev::kChunk - 1u) / dev::kChunk;
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint32_t* raws = reinterpret_cast<uint32_t*>(w);
+  uint32_t* qs = reinterpret_cast<uint32_t*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
+  uint32_t* qe = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 4u));
+  dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, raws, qs, qe,
+                    lc.counter};
+  dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, nullptr};
+  const uint32_t grid = grid_for(lc.num_cu, nc);  // >= 1: the waves also check the batch
+  if (lc.ev_start)
+    hipExtLaunchKernelGGL(dev::crc32c_region_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, lc.ev_start,
+                          nullptr, 0u, g, ka);
+  else
+    hipLaunchKernelGGL(dev::crc32c_region_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  dev::RegionFold f{reinterpret_cast<const uint8_t*>(O), rel0, offsets, lengths, n, init, init_all, flags, raws, qs,
+                    qe, lc.tables, out, lc.counter};
+  const dim3 fg((uint32_t)((n + 255u) / 256u));
+  if (lc.ev_stop)
+    hipExtLaunchKernelGGL(dev::crc32c_region_fold_kernel, fg, dim3(256), 0, lc.stream, nullptr, lc.ev_stop, 0u, f);
+  else
+    hipLaunchKernelGGL(dev::crc32c_region_fold_kernel, fg, dim3(256), 0, lc.stream, f);
+  return hipGetLastError();
 }
 
 }  // namespace nvl

@@ -192,8 +192,20 @@ class _Ref:
         lib.ref_crc32c_fixed_mt_reps.argtypes = [ctypes.c_void_p, ctypes.c_uint64,
                                                  ctypes.c_uint64, ctypes.c_uint64,
                                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
+        if hasattr(lib, "ref_dbbench_crc32c"):
+            lib.ref_dbbench_crc32c.restype = ctypes.c_uint64
+            lib.ref_dbbench_crc32c.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint32)]
         self.lib = lib
         self.path = path
+
+    def dbbench_crc32c(self, fn_addr=None, total: int = 500 * 1048576) -> tuple:
+        """db/db_bench.cc:729-746's crc32c loop (4 KiB Value() until `total`
+        bytes) on this thread: the reference's Value (fn_addr None) or the C
+        function at fn_addr with Value's signature.  (GiB/s, last crc)."""
+        crc = ctypes.c_uint32(0)
+        ns = self.lib.ref_dbbench_crc32c(fn_addr, total, ctypes.byref(crc))
+        done = (total + 4095) // 4096 * 4096
+        return done / (ns * 1e-9) / 2**30, crc.value
 
     def extend(self, init: int, data) -> int:
         b = bytes(data)

@@ -16,6 +16,8 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <pthread.h>
+#include <string.h>
+#include <time.h>
 #include "util/crc32c.h"
 
 namespace leveldb {
@@ -86,6 +88,38 @@ __attribute__((visibility("default")))
 int ref_crc32c_fixed_mt(const uint8_t* base, uint64_t stride, uint64_t len,
                         uint64_t n, uint32_t* out, int threads) {
   return ref_crc32c_fixed_mt_reps(base, stride, len, n, out, threads, 1);
+}
+
+// db/db_bench.cc:729-746 Crc32c(): Value() of ONE 4096-byte buffer of 'x'
+// until `total` bytes are checksummed, on the calling thread.  fn == NULL:
+// the reference's own leveldb::crc32c::Value (util/crc32c.h:20-22 inline ->
+// Extend, util/crc32c.cc:299-347 -> port::AcceleratedCRC32C); otherwise the
+// same loop through fn (e.g. the drop-in's nvl_crc32c_value).  Returns the
+// loop's wall time in ns (CLOCK_MONOTONIC); *crc = the last value.
+__attribute__((visibility("default")))
+uint64_t ref_dbbench_crc32c(uint32_t (*fn)(const void*, size_t), int64_t total, uint32_t* crc_out) {
+  const int size = 4096;
+  static char data[4096];
+  memset(data, 'x', sizeof(data));
+  (void)leveldb::crc32c::Value("", 0);  // resolve the static probe before timing
+  timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  int64_t bytes = 0;
+  uint32_t crc = 0;
+  if (fn) {
+    while (bytes < total) {
+      crc = fn(data, size);
+      bytes += size;
+    }
+  } else {
+    while (bytes < total) {
+      crc = leveldb::crc32c::Value(data, size);
+      bytes += size;
+    }
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (crc_out) *crc_out = crc;
+  return (uint64_t)(t1.tv_sec - t0.tv_sec) * 1000000000ull + (uint64_t)(t1.tv_nsec - t0.tv_nsec);
 }
 
 }  // extern "C"

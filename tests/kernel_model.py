@@ -403,3 +403,98 @@ def batch(mem: bytes, bufs, inits, nwaves: int):
             raise AssertionError("first portion not found")
         out[h[0]] = (~total) & 0xFFFFFFFF
     return out
+
+
+# ---- region path (nvl_crc32c_region_dev) -----------------------------------
+# A batch whose buffers lie in ONE region is checksummed over the region's
+# page-aligned 4 KiB chunks (crc32c_region_kernel) -- independent of where the
+# buffers start -- and each buffer is then derived from chunk-level values
+# (crc32c_region_fold_kernel).  Positions are relative to the grid origin
+# O = region & ~4095; chunk c covers [4096c, 4096c + 4096).
+
+REGION_DIRECT = 64  # buffers shorter than this are checksummed whole by the fold kernel
+
+
+def piece_raws(chunk: bytes):
+    return [raw_bytes(0, chunk[64 * l:64 * l + 64]) for l in range(64)]
+
+
+def masked_fold(lane_raws, L: int) -> int:
+    """Qe(L): the butterfly over the lanes below L (the others zeroed) -- the
+    chunk bytes [0, 64L) zero-extended to the chunk end."""
+    return wave_fold([v if l < L else 0 for l, v in enumerate(lane_raws)])
+
+
+def region_events(s: int, e: int, L: int):
+    """The (chunk, in-chunk offset) events a buffer [s, e) leaves for the
+    chunk kernel: its start unless on a chunk boundary, its end unless on one."""
+    ev = []
+    if L < REGION_DIRECT:
+        return ev
+    if s & 4095:
+        ev.append(("s", s >> 12, s & 4095))
+    if e & 4095:
+        ev.append(("e", (e - 1) >> 12, e - ((e - 1) >> 12 << 12)))
+    return ev
+
+
+def piece_prefix_raw(mem: bytes, p: int) -> int:
+    """R(p) = raw(0, bytes [p & ~63, p)): what the fold kernel re-reads."""
+    return raw_bytes(0, mem[p & ~63:p])
+
+
+def region_fold(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
+    """Extend(init, mem[s:s+L]) from the chunk raws and the events' Qe, as
+    crc32c_region_fold_kernel computes it (xp8[d] = x^(8d), xm8[d] = x^(-8d))."""
+    if L < REGION_DIRECT:
+        return (~raw_bytes((~init) & 0xFFFFFFFF, mem[s:s + L])) & 0xFFFFFFFF
+    e = s + L
+    c0, os_ = s >> 12, s & 4095
+    c1, oe = (e - 1) >> 12, e - ((e - 1) >> 12 << 12)
+    ninit = (~init) & 0xFFFFFFFF
+    qs = qe[("s", c0, os_)] if os_ else 0
+    rs = piece_prefix_raw(mem, s) if os_ else 0
+    # Ze'(s): bytes [cs0, s) at the chunk end, plus ~init injected at s
+    zs = qs ^ shift(rs ^ ninit, 4096 - os_)
+    if c0 == c1:
+        acc = zs
+    else:
+        acc = raws[c0] ^ zs
+        for c in range(c0 + 1, c1):
+            acc = apply_op(SH4096, acc) ^ raws[c]
+        acc = apply_op(SH4096, acc)
+    if oe == 4096:
+        v = acc ^ raws[c1]
+    else:
+        # unshift by 4096 - oe: multiply by x^(-8(4096-oe)), here as a check
+        d = 4096 - oe
+        v = unshift(acc ^ qe[("e", c1, oe)], d) ^ piece_prefix_raw(mem, e)
+    return (~v) & 0xFFFFFFFF
+
+
+def _xinv(v: int) -> int:
+    """v * x^-1 mod P (reflected): the inverse of one zero-bit feed."""
+    return (((v ^ POLY) << 1) | 1) & 0xFFFFFFFF if v & ONE else (v << 1) & 0xFFFFFFFF
+
+
+def unshift(v: int, nbytes: int) -> int:
+    for _ in range(8 * nbytes):
+        v = _xinv(v)
+    return v
+
+
+def region_batch(mem: bytes, bufs, inits):
+    """Every buffer of a region batch through the model: chunk pass (raws,
+    per-lane raws, Qe at each event's lane), then the per-buffer fold."""
+    NC = (len(mem) + 4095) // 4096
+    mem = mem + bytes(NC * 4096 - len(mem))
+    raws, lanes = [], []
+    for c in range(NC):
+        lr = piece_raws(mem[4096 * c:4096 * c + 4096])
+        lanes.append(lr)
+        raws.append(wave_fold(lr))
+    qe = {}
+    for s, L in bufs:
+        for kind, c, o in region_events(s, s + L, L):
+            qe[(kind, c, o)] = masked_fold(lanes[c], o >> 6)
+    return [region_fold(mem, raws, qe, s, L, i) for (s, L), i in zip(bufs, inits)]

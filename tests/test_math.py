@@ -170,3 +170,38 @@ def test_masked_pass_model(port, page_off):
         want = km.raw_bytes(0, bytes(4096 - L) + bytes(b ^ ((s >> (8 * q)) & 0xFF) if q < 4 else b
                                                        for q, b in enumerate(mem[p:p + L])))
         assert got == want, (p, L)
+
+
+def test_unshift_inverts_shift():
+    rng = random.Random(9)
+    for _ in range(40):
+        v = rng.getrandbits(32)
+        n = rng.randrange(0, 300)
+        assert km.unshift(km.shift(v, n), n) == v
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_region_path_model(port, seed):
+    """The region decomposition (page-aligned chunks, Qe at event lanes,
+    piece-prefix re-reads, per-buffer fold with ~init at the start) against
+    the oracle: packed, gapped, chunk- and piece-boundary starts/ends, tiny
+    buffers and multi-chunk buffers."""
+    rng = random.Random(100 + seed)
+    mem = bytes(port.fill(seed + 5, 0, 3 * 4096 * 4 + 512))
+    bufs, inits = [], []
+    p = rng.randrange(0, 200)
+    specials = [4096 - 3, 4096, 64, 63, 0, 1, 2, 3, 4097, 8192 + 5, 128]
+    while True:
+        L = specials.pop() if specials else rng.choice([rng.randrange(0, 70), rng.randrange(64, 5000),
+                                                       rng.randrange(4000, 9000)])
+        if p + L > len(mem):
+            break
+        bufs.append((p, L))
+        inits.append(rng.getrandbits(32) if rng.random() < 0.5 else 0)
+        p += L + rng.choice([0, 0, 4, 5, 1, 64 - (p + L) % 64])
+    # starts/ends exactly on piece and chunk boundaries
+    bufs += [(4096, 64), (4096 * 2 - 64, 64 + 4096)]
+    inits += [0, 7]
+    got = km.region_batch(mem, bufs, inits)
+    want = [port.extend(i, mem[s:s + L]) for (s, L), i in zip(bufs, inits)]
+    assert got == want

@@ -2,6 +2,7 @@
 around each call, median of R reps), every result checked.
     python tools/bench_configs.py [--lib build/libnvl_crc32c_X.so] [--configs 2,3,4,v,g,r]
   2, 3, 4  BASELINE configs 2-4 (golden digests)
+  3R, vR, rR  config 3, v and r through nvl_crc32c_region_dev (the region path)
   v        10^5 x 4097 B at stride 4101: block | type of 4096-byte SSTable blocks with their
            4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
   g        10^5 x 4096 B at stride 4099 from an odd base: the fixed-stride general path
@@ -43,12 +44,18 @@ def timeit(fn, reps):
     return float(np.median([ev[2*j].elapsed_time(ev[2*j+1]) for j in range(reps)])) * 1e-3
 
 
-def varlen(offs, lens, total, seed):
+def varlen(offs, lens, total, seed, region=False):
     n = lens.size
     buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
     lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, seed, None)
     o = torch.from_numpy(offs.astype(np.int64)).to(dev); m = torch.from_numpy(lens.astype(np.int64)).to(dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
+    if region:  # nvl_crc32c_region_dev over the region [buf, buf + total)
+        wsb = lib.nvl_crc32c_region_workspace_bytes(total, n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fn = lambda: lib.nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.data_ptr(), None, 0,
+                                               out.data_ptr(), n, 0, ws.data_ptr(), wsb, st)
+        return buf, out, fn, (o, m, ws)
     wsb = lib.nvl_crc32c_batch_workspace_bytes(n)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     fn = lambda: lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0,
@@ -68,23 +75,23 @@ for c in a.configs.split(","):
         fn = lambda: lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(), wsb, st)
         alg = n * (L + 4)
         check = lambda res: p.digest(res) == cfg["digest"]
-    elif c == "3":
+    elif c in ("3", "3R"):
         cfg = g["cfg3"]; total = cfg["total"]
         lens = p.cfg3_lengths(cfg["len_seed"], total)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
         n = lens.size
-        buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"])
+        buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"], region=c == "3R")
         alg = total + 12 * n
         check = lambda res: p.digest(res) == cfg["digest"]
-    elif c in ("v", "r"):
+    elif c in ("v", "r", "vR", "rR"):
         n = 100_000
-        if c == "v":
+        if c[0] == "v":
             lens = np.full(n, 4097, dtype=np.int64)
         else:
             lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
         offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
         total = int(offs[-1] + lens[-1]) + 4
-        buf, out, fn, keep = varlen(offs, lens, total, 0x5EED00B1)
+        buf, out, fn, keep = varlen(offs, lens, total, 0x5EED00B1, region=c.endswith("R"))
         alg = int(lens.sum()) + 20 * n
         host = buf.cpu().numpy()
         check = lambda res: bool(np.array_equal(res, p.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64))))

@@ -392,14 +392,24 @@ def main():
     res = crc32c.to_u32(out)
     with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
         golden = json.load(f)
-    if args.config == "cfg5" or (N == 1 and n_local == 100_000):
-        # every rank's CRCs in global order -> digest = Value() of the
-        # little-endian CRC array, golden from the oracle pinned
-        # to the reference (tests/golden/configs.json)
+    union = golden.get("cfg2_union", {}).get(str(N)) if args.config == "cfg2" and n_local == 100_000 else None
+    if N > 1 and (args.config == "cfg5" or union):
+        # every rank's own digest (cfg2: golden per-rank digests of the
+        # weak-scaling union, global blocks 0..N*10^5-1) and the gathered
+        # global digest (shard.verify_shards: ONE all_gather of the 4-byte
+        # results; tests/test_dist.py drives the same function over gloo)
+        g = golden["cfg5"] if args.config == "cfg5" else union
+        v = shard.verify_shards(out[:n_local].to(red_dev), total, g)
+        if rank == 0:
+            verify.update(v)
+            verify["crc0_ok"] = int(v["crc0"], 16) == golden[args.config if args.config == "cfg5" else "cfg2"][
+                "crc_first"][0]
+    elif args.config == "cfg5" or (N == 1 and n_local == 100_000):
+        # the CRCs in global order -> digest = Value() of the little-endian
+        # CRC array, golden from the reference build
+        # (tests/golden/configs.json)
         g = golden[args.config]
-        # (shard.gather_crcs: ONE all_gather of the padded 4-byte results;
-        # tests/test_dist.py runs the same call over gloo)
-        allc = shard.gather_crcs(out[:n_local].to(red_dev), total) if N > 1 else res
+        allc = res
         if rank == 0:
             d = crc32c.value(np.ascontiguousarray(allc, dtype="<u4").tobytes())
             verify.update({"crc0": hex(int(allc[0])), "crc0_ok": int(allc[0]) == g["crc_first"][0],

@@ -59,3 +59,31 @@ def digest(crcs: np.ndarray) -> int:
     computed with the engine's host path."""
     from . import crc32c
     return crc32c.value(np.ascontiguousarray(crcs, dtype="<u4").view(np.uint8))
+
+
+def verify_shards(local, n_total: int, expect: dict, group=None) -> dict:
+    """Check every rank's CRCs of a round-robin batch (outside any timed
+    region).  local: this rank's int32 CRC tensor in local order; expect:
+    a golden entry with "digest" (over all n_total CRCs in global order) and,
+    optionally, "rank_digests" (each rank's own digest over its blocks in
+    local order) and "crc_last".  Every rank checks its own digest (the
+    verdicts are AND-reduced, so rank 0 learns about every rank), then the
+    slices are all-gathered (gather_crcs) and the global digest checked.
+    Returns the same dict on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    mine = local.detach().cpu().numpy().view(np.uint32)
+    rd = expect.get("rank_digests")
+    own_ok = rd is not None and rank < len(rd) and digest(mine) == rd[rank]
+    flag = torch.tensor([1 if own_ok else 0], dtype=torch.int32, device=local.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    full = gather_crcs(local, n_total, group)
+    d = digest(full)
+    out = {"rank_digests_ok": bool(flag.item()) if rd is not None else None,
+           "digest": hex(d), "digest_ok": d == expect["digest"], "blocks_checked": int(full.size),
+           "crc0": hex(int(full[0])) if full.size else None}
+    if "crc_last" in expect and full.size:
+        out["crc_last_ok"] = int(full[-1]) == expect["crc_last"]
+    return out

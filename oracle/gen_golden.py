@@ -267,6 +267,33 @@ def cfg5() -> dict:
                    "10^5-block chunk incl. the prefix, identical"}
 
 
+def cfg2_union() -> dict:
+    """Config 2 at N GPUs (bench.py's weak scaling: 10^5 blocks PER rank,
+    rank r holding global blocks r, r + N, r + 2N, ...): the union is global
+    blocks 0 .. N*10^5 - 1 of the config-2 stream (seed 0x5EED0001).  For N =
+    2, 4 and 8: the digest of all N*10^5 CRCs in global order (what rank 0
+    checks after shard.gather_crcs) and each rank's own digest over its
+    blocks in local order (what every rank checks by itself).  CRCs by the
+    REFERENCE's own build (oracle/_ref), in 10^5-block slices."""
+    p = oracle.port()
+    r = oracle.ref("sse")
+    per, L, nmax = 100_000, 4096, 8
+    th = min(8, os.cpu_count() or 1)
+    crc = np.empty(per * nmax, dtype=np.uint32)
+    part = aligned_buffer(per * L)
+    for s in range(0, per * nmax, per):
+        part[:] = p.fill(0x5EED0001, s * L, part.size)
+        crc[s:s + per] = r.fixed_mt(part, L, L, per, th)
+    out = {"seed": 0x5EED0001, "blocks_per_rank": per, "len": L,
+           "how": "reference build (oracle/_ref, util/crc32c.cc + port/port_posix_sse.cc) over global blocks "
+                  "0 .. 8*10^5-1; digest = Value() of the little-endian CRC array"}
+    for N in (2, 4, 8):
+        u = crc[:per * N]
+        out[str(N)] = {"digest": p.digest(u), "crc_last": int(u[-1]),
+                       "rank_digests": [p.digest(u[k::N]) for k in range(N)]}
+    return out
+
+
 def table_cases() -> dict:
     """SSTable scenarios (tests/table_cases.py) scanned by the REFERENCE's own
     Footer::DecodeFrom, ReadBlock and Block::Iter (table/format.cc,
@@ -312,14 +339,23 @@ def main() -> None:
         with open(path, "w") as f:
             json.dump(d, f, indent=1)
         print("cfg5 digest", hex(d["cfg5"]["digest"]), "crc_last", hex(d["cfg5"]["crc_last"]))
+    if "cfg2_union" in only:  # added to the existing configs.json
+        path = os.path.join(GOLDEN, "configs.json")
+        with open(path) as f:
+            d = json.load(f)
+        d["cfg2_union"] = cfg2_union()
+        with open(path, "w") as f:
+            json.dump(d, f, indent=1)
+        print("cfg2_union", {k: hex(v["digest"]) for k, v in d["cfg2_union"].items() if isinstance(v, dict)})
     if only and "configs" not in only:
         return
     d = configs(not args.no_cfg4)
-    try:  # keep a cfg5 made earlier (--only cfg5)
+    try:  # keep cfg5 / cfg2_union made earlier (--only cfg5,cfg2_union)
         with open(os.path.join(GOLDEN, "configs.json")) as f:
             old = json.load(f)
-        if "cfg5" in old:
-            d["cfg5"] = old["cfg5"]
+        for k in ("cfg5", "cfg2_union"):
+            if k in old:
+                d[k] = old[k]
     except (OSError, ValueError):
         pass
     d["provenance"] = provenance

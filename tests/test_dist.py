@@ -77,6 +77,75 @@ def test_round_robin_gather_matches_single_process(world, n):
         assert whole[:8].tolist() == g["crc_first"]
 
 
+def _verify_worker(rank, world, port, per, expect, result_q):
+    """One rank of bench.py's N > 1 verification (shard.verify_shards) on the
+    CPU: rank r checksums its round-robin shard (global blocks r, r+N, ...,
+    `per` of them) with the engine's host path and verifies it."""
+    import torch.distributed as dist
+    import oracle
+    from nvlevelz_amd import crc32c, shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = 4096
+        n = per * world
+        whole = oracle.port().fill(0x5EED0001, 0, n * L).reshape(n, L)
+        mine = np.ascontiguousarray(whole[rank::world])
+        del whole
+        local = np.array([crc32c.value(mine[k]) for k in range(per)], dtype=np.uint32)
+        if rank == 1 and expect.get("corrupt_rank1"):
+            local[per // 2] ^= 1
+        v = shard.verify_shards(torch.from_numpy(local.view(np.int32).copy()), n, expect)
+        result_q.put((rank, v))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_verify(world, per, expect):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_verify_worker, args=(r, world, port, per, expect, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    return res
+
+
+def test_verify_shards_cfg2_union_world2():
+    """bench.py --gpus 2's verification on the weak-scaling union (2 x 10^5
+    blocks): both ranks' own digests and the gathered digest equal the
+    reference-built goldens (tests/golden/configs.json cfg2_union)."""
+    g = load_golden("configs")["cfg2_union"]["2"]
+    res = _run_verify(2, 100_000, g)
+    for r, v in res.items():
+        assert v["rank_digests_ok"] is True and v["digest_ok"] is True and v["crc_last_ok"] is True, (r, v)
+        assert v["blocks_checked"] == 200_000
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_verify_shards_world3(corrupt):
+    """World size 3 (no golden: expectations from the oracle); one flipped
+    CRC on rank 1 fails rank 1's own digest, which every rank then reports
+    (AND-reduced), and the global digest."""
+    import oracle
+    p = oracle.port()
+    per, world = 700, 3
+    n = per * world
+    whole = p.fixed(p.fill(0x5EED0001, 0, n * 4096), 4096, 4096, n)
+    exp = {"digest": p.digest(whole), "crc_last": int(whole[-1]),
+           "rank_digests": [p.digest(whole[r::world]) for r in range(world)], "corrupt_rank1": corrupt}
+    res = _run_verify(world, per, exp)
+    for r, v in res.items():
+        assert v["rank_digests_ok"] is (not corrupt), (r, v)
+        assert v["digest_ok"] is (not corrupt), (r, v)
+
+
 def test_partition_math():
     from nvlevelz_amd import shard
     for n in (0, 1, 7, 100000, 10_000_000):

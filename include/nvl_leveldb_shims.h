@@ -595,7 +595,9 @@ class TableReader {
     std::vector<size_t> meta;
     for (size_t i = 0; i < blocks_.size(); ++i) {
       if (blocks_[i].role == NVL_TBLOCK_DATA) data_.push_back(i);
-      if (blocks_[i].role == NVL_TBLOCK_META) meta.push_back(i);
+      // (a metaindex value that is not a handle is listed as BAD_HANDLE with
+      // offset = size = 0: nothing to read, as BlockReader's "bad block handle")
+      if (blocks_[i].role == NVL_TBLOCK_META && blocks_[i].verdict == NVL_BLOCK_UNCHECKED) meta.push_back(i);
     }
     return Check(meta);
   }

@@ -114,7 +114,10 @@ def build(port, spec: dict) -> tuple[bytes, dict]:
     for m in range(spec.get("nmeta", 1)):
         filt = port.fill(spec["seed"] * 31 + m, 0, int(rng.integers(0, 600))).tobytes()
         meta.append((b"filter.leveldb.BuiltinBloomFilter%d" % (m + 2), w.raw(filt)))
-    meta_h = w.raw(block([(k, handle(*h)) for k, h in meta], 16))
+    ments = [(k, handle(*h)) for k, h in meta]
+    if spec.get("meta_mode") == "bad_handle" and ments:  # a metaindex value that is not a BlockHandle
+        ments[0] = (ments[0][0], b"\xff")
+    meta_h = w.raw(block(ments, 16))
     mode = spec.get("index_mode", "")
     ents = [(k, handle(*h)) for h, k in data]
     if mode == "bad_handle" and ents:      # a value that is not a BlockHandle (table.cc:160-165)
@@ -235,6 +238,7 @@ def named() -> list[dict]:
     add("compressed_index", index_mode="compressed")
     add("restart0_past", index_mode="restart0_past", nblocks=1)
     add("varint32_wrap", index_mode="varint32_wrap", nblocks=5)
+    add("meta_bad_handle", meta_mode="bad_handle", nmeta=2)
     return c
 
 

@@ -35,8 +35,8 @@ HOST = 0x100
 def shim():
     from nvlevelz_amd import _lib  # noqa: F401  (loads libnvl_crc32c.so first)
     path = os.path.join(NATIVE, "libshim_harness.so")
-    if not os.path.exists(path):
-        subprocess.run(["make", "-s", "-C", NATIVE], check=True)
+    if not os.path.exists(path) or os.path.isdir("/root/reference"):  # rebuilt when stale here
+        subprocess.run(["make", "-s", "-C", NATIVE, "libshim_harness.so"], check=True)
     lib = ctypes.CDLL(path)
     vp, u64, sz, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32
     lib.shim_log_write.restype = ctypes.c_int

@@ -30,7 +30,23 @@
 extern "C" {
 #endif
 
-#define NVL_FRAMING_HOST 0x100u /* compute CRCs with the host CRC instead of the GPU */
+/* Engine of a host-resident call's CRC batch.  flags = 0 chooses by size:
+ * batches of fewer than nvl_framing_gpu_min_bytes() checksummed bytes run on
+ * the calling thread's host CRC (nvl_crc32c_extend), larger ones on the GPU
+ * (one staging copy, H2D, one batch kernel, D2H) -- the crossover measured at
+ * the fork's call-site sizes (profiles/r04_shim_latency.jsonl);
+ * the environment variable NVL_FRAMING_GPU_MIN_BYTES overrides it.  The two
+ * flags force an engine.  A GPU batch that fails returns its error; no call
+ * ever falls back to the other engine.  (nvl_sstable_verify_table_dev's image
+ * is in HBM already: always the GPU.) */
+#define NVL_FRAMING_HOST 0x100u /* compute CRCs with the host CRC */
+#define NVL_FRAMING_GPU 0x400u  /* compute CRCs on the GPU whatever the size */
+
+/* The crossover in bytes (flags = 0: GPU at or above it). */
+NVL_API uint64_t nvl_framing_gpu_min_bytes(void);
+/* 1 if a host-resident batch of `crc_bytes` checksummed bytes runs on the GPU
+ * under `flags`, 0 if on the host CRC, NVL_CRC32C_EINVAL for both flags. */
+NVL_API int nvl_framing_uses_gpu(uint64_t crc_bytes, uint32_t flags);
 
 /* ---- SSTable blocks ------------------------------------------------------ */
 

@@ -65,7 +65,7 @@ class LogReader {
   };
 
   // log_reader.h:32-44.  `file` must stay live while the reader is used;
-  // `flags` may hold NVL_FRAMING_HOST.
+  // `flags`: 0 = the size policy (nvl_framing_uses_gpu), NVL_FRAMING_HOST / NVL_FRAMING_GPU force an engine.
   LogReader(const char* file, uint64_t file_len, Reporter* reporter, bool checksum, uint64_t initial_offset,
             uint32_t flags = 0)
       : file_(file),
@@ -490,7 +490,7 @@ template <class WritableFileT, class SliceT, class StatusT>
 class BatchingWritableFile : public WritableFileT, public DeferredBlockCrc {
  public:
   // target: receives every sealed byte (not owned; Close() closes it).
-  // flags: NVL_FRAMING_HOST for the host CRC.
+  // flags: 0 = the size policy; NVL_FRAMING_HOST / NVL_FRAMING_GPU force the host CRC / the GPU.
   explicit BatchingWritableFile(WritableFileT* target, uint64_t seal_bytes = 64ull << 20, uint32_t flags = 0)
       : target_(target), seal_bytes_(seal_bytes), flags_(flags) {}
 

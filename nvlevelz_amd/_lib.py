@@ -58,6 +58,8 @@ SIGNATURES = {
                                            _vp]),
     "nvl_crc32c_region_workspace_bytes": (_sz, [_u64, _u64]),
     # include/nvl_framing.h
+    "nvl_framing_gpu_min_bytes": (_u64, []),
+    "nvl_framing_uses_gpu": (_int, [_u64, _u32]),
     "nvl_sstable_seal_trailers": (_int, [_vp, _u64, _vp, _sz, _u32]),
     "nvl_sstable_verify_blocks": (_int, [_vp, _u64, _vp, _sz, _vp, _vp, _u32]),
     "nvl_log_scan": (_int, [_vp, _u64, _u64, _int, _vp, _sz, _vp, _u32]),
@@ -67,6 +69,7 @@ SIGNATURES = {
 }
 
 FRAMING_HOST = 0x100
+FRAMING_GPU = 0x400
 BLOCK_OK, BLOCK_TRUNCATED, BLOCK_CHECKSUM_MISMATCH, BLOCK_BAD_TYPE = 0, 1, 2, 3
 LOG_RECORD, LOG_BAD_LENGTH, LOG_CHECKSUM, LOG_ZERO, LOG_EOF = 0, 1, 2, 3, 4
 BLOCK_BAD_HANDLE = 4

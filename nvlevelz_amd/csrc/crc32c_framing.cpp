@@ -6,6 +6,7 @@
 // (nvl_crc32c_batch_region_host) unless NVL_FRAMING_HOST asks for the host
 // CRC explicitly.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -14,6 +15,12 @@
 #include "crc32c_internal.h"
 #include "crc32c_math.h"
 #include "nvl_framing.h"
+
+// flags = 0 crossover (bytes checksummed per host-resident call), from
+// profiles/r04_shim_latency.jsonl.
+#ifndef NVL_FRAMING_DEFAULT_GPU_MIN_BYTES
+#define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES (8ull << 20)
+#endif
 
 namespace nvl {
 namespace {
@@ -29,14 +36,41 @@ inline void store_le32(uint8_t* p, uint32_t v) {
   p[3] = (uint8_t)(v >> 24);
 }
 
-// crc[i] = Value(region[off[i] .. off[i]+len[i])): one GPU batch, or the host
-// CRC when the caller selected it.
+// Host-resident batches smaller than this run on the calling thread's host
+// CRC when flags = 0 (the measured crossover).
+constexpr uint64_t kGpuMinBytes = NVL_FRAMING_DEFAULT_GPU_MIN_BYTES;
+
+uint64_t gpu_min_bytes() {
+  static const uint64_t v = [] {
+    const char* e = getenv("NVL_FRAMING_GPU_MIN_BYTES");
+    if (!e || !*e) return kGpuMinBytes;
+    char* end = nullptr;
+    const unsigned long long x = strtoull(e, &end, 0);
+    return (end && *end == '\0') ? (uint64_t)x : kGpuMinBytes;
+  }();
+  return v;
+}
+
+// 1 GPU, 0 host, NVL_CRC32C_EINVAL for contradictory flags.
+int uses_gpu(uint64_t bytes, uint32_t flags) {
+  if ((flags & NVL_FRAMING_HOST) && (flags & NVL_FRAMING_GPU)) return NVL_CRC32C_EINVAL;
+  if (flags & NVL_FRAMING_HOST) return 0;
+  if (flags & NVL_FRAMING_GPU) return 1;
+  return bytes >= gpu_min_bytes() ? 1 : 0;
+}
+
+// crc[i] = Value(region[off[i] .. off[i]+len[i])): one GPU batch or the host
+// CRC, by uses_gpu().
 int value_many(const uint8_t* region, uint64_t region_len, const std::vector<uint64_t>& off,
                const std::vector<uint64_t>& len, std::vector<uint32_t>* crc, uint32_t flags) {
   const size_t n = off.size();
   crc->assign(n, 0u);
+  uint64_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) bytes += len[i];
+  const int g = uses_gpu(bytes, flags);
+  if (g < 0) return g;
   if (n == 0) return NVL_CRC32C_OK;
-  if (flags & NVL_FRAMING_HOST) {
+  if (!g) {
     for (size_t i = 0; i < n; ++i) (*crc)[i] = host_extend(0, region + off[i], len[i]);
     return NVL_CRC32C_OK;
   }
@@ -130,6 +164,11 @@ uint32_t block_handles(const uint8_t* data, uint64_t size, std::vector<nvl_block
 using namespace nvl;
 
 extern "C" {
+
+uint64_t nvl_framing_gpu_min_bytes(void) { return nvl::gpu_min_bytes(); }
+
+int nvl_framing_uses_gpu(uint64_t crc_bytes, uint32_t flags) { return nvl::uses_gpu(crc_bytes, flags); }
+
 
 int nvl_sstable_seal_trailers(void* file, uint64_t file_len, const nvl_block_handle* blocks, size_t n,
                               uint32_t flags) {

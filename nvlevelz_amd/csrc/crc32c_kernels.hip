@@ -2774,6 +2774,22 @@ __device__ __forceinline__ Win make_win(const RegionGeom& g, const WinRaw& r, ui
 // 64-ary search, one wave-wide load per level.
 __device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane) {
   uint64_t lo = 0, hi = g.n;  // every b < lo has e_b <= A; the answer is <= hi
+  {  // first a window at the interpolated index (a packed region of similar buffers: one load)
+    const double f = (double)A / (double)(g.rel0 + g.region_len + 1u);
+    const uint64_t gi = min((uint64_t)(f * (double)g.n), g.n - 1u);
+    const uint64_t w0 = gi > 32u ? gi - 32u : 0u;
+    const uint64_t b = min(w0 + (uint64_t)lane, g.n - 1u);
+    const uint64_t e = g.rel0 + ldg64(g.offsets, b) + ldg64(g.lengths, b);
+    const uint64_t m = __ballot(w0 + (uint64_t)lane < g.n && e > A);
+    if (m & 1u) {
+      if (w0 == 0) return 0;
+      hi = w0;  // the answer lies below the window
+    } else if (m) {
+      return w0 + (uint64_t)__builtin_ctzll(m);
+    } else {
+      lo = min(w0 + 64u, g.n);  // above it
+    }
+  }
   while (hi - lo > 64u) {
     const uint64_t step = (hi - lo + 63u) / 64u;
     const uint64_t b = min(lo + (uint64_t)lane * step, hi - 1u);
@@ -2826,6 +2842,57 @@ __device__ __forceinline__ void chains_keep(const uint8_t* lds, const LaneBase& 
   for (int u = 0; u < U; ++u) raw[u] = crc[u];
 }
 
+// The same with each chunk's first event fused in: besides raw[u], the
+// butterfly over the lanes below Lf[u] (the others zeroed) = Qe at the
+// chunk's first event lane, interleaved with the full butterflies (Lf = 0
+// when the chunk has no event: Qf = 0).
+template <int U>
+__device__ __forceinline__ void chains_first(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
+                                             int lane, const uint32_t (&Lf)[U], uint32_t (&lr)[U],
+                                             uint32_t (&raw)[U], uint32_t (&qf)[U]) {
+  uint32_t crc[2 * U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) crc[u] = w[u][0];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    lr[u] = crc[u];
+    crc[U + u] = (uint32_t)lane < Lf[u] ? crc[u] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<0, 0, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<1, 1, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<2, 2, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<3, 3, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<4, 4, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<5, 5, false>(lds, crc[u], lane);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    raw[u] = crc[u];
+    qf[u] = uniform_u32(crc[U + u]);
+  }
+}
+
+// Event masks of a window over the unit's byte range [A, B): starts and
+// ends of big buffers strictly inside a chunk.
+struct EvMasks {
+  uint64_t ms, me;
+};
+__device__ __forceinline__ EvMasks event_masks(const Win& w, uint64_t A, uint64_t B) {
+  const bool sv = w.big && (w.s & (kChunk - 1u)) != 0u && w.s >= A && w.s < B;
+  const bool ev = w.big && (w.e & (kChunk - 1u)) != 0u && w.e > A && w.e < B;
+  return EvMasks{__ballot(sv), __ballot(ev)};
+}
+
 // Qe(L): the butterfly over the lanes below L, the others zeroed.
 __device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr, uint32_t L, int lane) {
   uint32_t g = (uint32_t)lane < L ? lr : 0u;
@@ -2845,13 +2912,13 @@ __device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr,
 // buffer of the current one still starts before the unit's end.
 template <int U>
 __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t* lds, Win w, uint64_t cur,
-                                              uint64_t ca, uint32_t cu, const uint32_t (&lr)[U], int lane) {
+                                              uint64_t ca, uint32_t cu, const uint32_t (&lr)[U],
+                                              const uint32_t (&Lf)[U], const uint32_t (&qf)[U], EvMasks em,
+                                              int lane) {
   const uint64_t A = ca * kChunk, B = (ca + cu) * kChunk;
   uint32_t pk = ~0u, pL = ~0u, pq = 0;
   for (;;) {
-    const bool sv = w.big && (w.s & (kChunk - 1u)) != 0u && w.s >= A && w.s < B;
-    const bool ev = w.big && (w.e & (kChunk - 1u)) != 0u && w.e > A && w.e < B;
-    const uint64_t ms = __ballot(sv), me = __ballot(ev);
+    const uint64_t ms = em.ms, me = em.me;
     uint64_t all = ms | me;
     while (all) {
       const uint32_t j = (uint32_t)__builtin_ctzll(all);
@@ -2862,10 +2929,14 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t
         const uint32_t pos = (uint32_t)(lane_u64(t ? w.e : w.s, j) - A);
         const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6;
         if (k != pk || L != pL) {
-          uint32_t v = lr[0];
+          uint32_t v = lr[0], lf = Lf[0], q0 = qf[0];
 #pragma unroll
-          for (int q = 1; q < U; ++q) v = k == (uint32_t)q ? lr[q] : v;
-          pq = masked_fold(lds, v, L, lane);
+          for (int q = 1; q < U; ++q) {
+            v = k == (uint32_t)q ? lr[q] : v;
+            lf = k == (uint32_t)q ? Lf[q] : lf;
+            q0 = k == (uint32_t)q ? qf[q] : q0;
+          }
+          pq = L == lf ? q0 : masked_fold(lds, v, L, lane);  // the first event lane came with the butterflies
           pk = k;
           pL = L;
         }
@@ -2875,6 +2946,33 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t
     if (cur + 64u >= g.n || lane_u64(w.s, 63) >= B) break;
     cur += 64u;  // the unit's buffers run past the window (short buffers): the next one
     w = make_win(g, load_win(g, cur, lane), cur, lane);
+    em = event_masks(w, A, B);
+  }
+}
+
+// First event lane per chunk of the unit (64: none) from the window's masks.
+template <int U>
+__device__ __forceinline__ void first_lanes(const Win& w, const EvMasks& em, uint64_t ca, uint32_t (&Lf)[U]) {
+  const uint64_t A = ca * kChunk;
+#pragma unroll
+  for (int k = 0; k < U; ++k) Lf[k] = 0u;
+  uint64_t all = em.ms | em.me;
+  uint32_t need = (1u << U) - 1u;
+  while (all && need) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(all);
+    all &= all - 1u;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (!(((t ? em.me : em.ms) >> j) & 1u)) continue;
+      const uint32_t pos = (uint32_t)(lane_u64(t ? w.e : w.s, j) - A);
+      const uint32_t k = pos >> 12;
+      if ((need >> k) & 1u) {
+#pragma unroll
+        for (int q = 0; q < U; ++q)
+          if ((uint32_t)q == k) Lf[q] = (pos & (kChunk - 1u)) >> 6;
+        need &= ~(1u << k);
+      }
+    }
   }
 }
 
@@ -2934,7 +3032,10 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     Chunk nxt[U];
     load_unit(can, cun, nxt);
 
-    uint32_t lr[U], raw[U];
+    const EvMasks em = event_masks(w, ca * kChunk, (ca + cu) * kChunk);
+    uint32_t Lf[U];
+    first_lanes<U>(w, em, ca, Lf);
+    uint32_t lr[U], raw[U], qf[U];
     if (cu == (uint32_t)U) {
       uint32_t wd[U][16];
 #pragma unroll
@@ -2943,17 +3044,18 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
         row_transpose(wd[k]);
       }
-      chains_keep<U>(lds, lb, wd, lane, lr, raw);
+      chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf);
     } else {  // the range's single-chunk units
-      uint32_t wd[1][16], l1[1], r1[1];
+      uint32_t wd[1][16], l1[1], r1[1], f1[1] = {Lf[0]}, q1[1];
 #pragma unroll
       for (int q = 0; q < 16; ++q) wd[0][q] = cur[0].d[q];
       row_transpose(wd[0]);
-      chains_keep<1>(lds, lb, wd, lane, l1, r1);
+      chains_first<1>(lds, lb, wd, lane, f1, l1, r1, q1);
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         lr[k] = l1[0];
         raw[k] = r1[0];
+        qf[k] = q1[0];
       }
     }
     if (lane == 0) {
@@ -2961,7 +3063,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
       for (int k = 0; k < U; ++k)
         if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
     }
-    region_events<U>(g, lds, w, cursor, ca, cu, lr, lane);
+    region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, em, lane);
 
     u = un;
     ca = can;
@@ -3025,18 +3127,32 @@ __device__ uint32_t serial_raw(const uint32_t* t, uint32_t crc, const uint8_t* p
   return crc;
 }
 
-// R(p) = raw(0, grid bytes [p & ~63, p)): a prefix of one 64-byte piece
-// (64-byte aligned: the grid origin is page-aligned).
-__device__ __forceinline__ uint32_t piece_prefix(const uint32_t* t, const uint8_t* grid, uint64_t p) {
-  const uint32_t o = (uint32_t)(p & 63u);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(grid + (p & ~(uint64_t)63));
-  uint32_t crc = 0;
-  for (uint32_t k = 0; k < (o >> 2); ++k) crc = fold_slice4(t, crc ^ w[k]);
-  if (o & 3u) {
-    const uint32_t x = w[o >> 2];
-    for (uint32_t b = 0; b < (o & 3u); ++b) crc = fold_step1(t, crc, (x >> (8u * b)) & 255u);
+// R = raw(0, the first o bytes of a 64-byte piece) from its 16 words, with
+// a fixed trip count (no divergence, every load issued up front).
+__device__ __forceinline__ uint32_t piece_prefix(const uint32_t* t, const u32x4 (&v)[4], uint32_t o) {
+  const uint32_t q = o >> 2, r = o & 3u;
+  uint32_t crc = 0, x = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t k = 4u * (uint32_t)j + (uint32_t)m;
+      const uint32_t w = v[j][m];
+      const uint32_t nx = fold_slice4(t, crc ^ w);
+      x = k == q ? w : x;
+      crc = k < q ? nx : crc;
+    }
+  }
+#pragma unroll
+  for (uint32_t b = 0; b < 3u; ++b) {
+    const uint32_t nx = fold_step1(t, crc, (x >> (8u * b)) & 255u);
+    crc = b < r ? nx : crc;
   }
   return crc;
+}
+
+__device__ __forceinline__ uint32_t fold_sh4096(const uint32_t* sh, uint32_t acc) {
+  return sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)];
 }
 
 __global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
@@ -3059,21 +3175,38 @@ __global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
     } else {
       const uint64_t e = s + L;
       const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
-      const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));
-      uint32_t zs = gf_mul(a.tables[kTabXp8 + kChunk - os], (os ? piece_prefix(sl, a.grid, s) : 0u) ^ ninit);
-      if (os) zs ^= a.qs[i];
+      const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
+      // every load first: the two pieces (the end's clamped into the grid
+      // when it is a chunk end), the events' Qe, the end chunks' raws, the powers
+      const uintptr_t gs = (uintptr_t)a.grid + (s & ~(uint64_t)63);
+      const uintptr_t ge = (uintptr_t)a.grid + (oe == kChunk ? e - 64u : (e & ~(uint64_t)63));
+      u32x4 vs[4], ve[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vs[j] = ld16c(gs + 16u * (uint32_t)j);
+        ve[j] = ld16c(ge + 16u * (uint32_t)j);
+      }
+      const uint32_t q_s = a.qs[i], q_e = a.qe[i], r0 = a.raws[c0], r1 = a.raws[c1];
+      const uint32_t xs = a.tables[kTabXp8 + kChunk - os], xe = a.tables[kTabXm8 + (kChunk - oe)];
+      // Ze'(s) = Qe(s) ^ (R(s) ^ ~init) x^(8(4096 - os)): bytes [cs0, s) and ~init at s, at the chunk end
+      const uint32_t zs = (os ? q_s : 0u) ^ gf_mul(xs, piece_prefix(sl, vs, s & 63u) ^ ninit);
       uint32_t acc = zs;
       if (c0 != c1) {
-        acc ^= a.raws[c0];
-        for (uint64_t c = c0 + 1u; c < c1; ++c)
-          acc = sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^
-                sh[768u + (acc >> 24)] ^ a.raws[c];
-        acc = sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)];
+        acc ^= r0;
+        for (uint64_t c = c0 + 1u; c < c1; c += 4u) {  // the chunks in between, four loads at a time
+          uint32_t rr[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) rr[k] = a.raws[min(c + (uint64_t)k, c1)];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (c + (uint64_t)k < c1) acc = fold_sh4096(sh, acc) ^ rr[k];
+        }
+        acc = fold_sh4096(sh, acc);
       }
-      if (oe == kChunk)
-        v = acc ^ a.raws[c1];
-      else
-        v = gf_mul(a.tables[kTabXm8 + kChunk - oe], acc ^ a.qe[i]) ^ piece_prefix(sl, a.grid, e);
+      // a chunk-end e: the whole chunk, no unshift (xe = x^0)
+      const uint32_t ze = oe == kChunk ? r1 : q_e;
+      const uint32_t re = oe == kChunk ? 0u : piece_prefix(sl, ve, e & 63u);
+      v = gf_mul(xe, acc ^ ze) ^ re;
     }
     a.out[i] = finish(~v, a.flags);
   }

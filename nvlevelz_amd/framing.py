@@ -1,6 +1,8 @@
 """Python view of the call-site shims (include/nvl_framing.h): SSTable block
 trailers, block and whole-table verification, log scan and log sealing, each
-one CRC batch on the GPU (or the host CRC with ``host=True``).
+one CRC batch: by default the library's size policy picks the calling
+thread's host CRC or the GPU (nvl_framing_uses_gpu);
+``host=True`` forces the host CRC, ``host=False`` the GPU.
 
 Verdicts carry the reference's Status texts, so a caller can report them the
 way LevelDB does:
@@ -20,7 +22,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass
-from typing import List, Sequence, Tuple, Union
+from typing import Optional, List, Sequence, Tuple, Union
 
 import numpy as np
 
@@ -55,8 +57,12 @@ class FramingError(RuntimeError):
         self.rc = rc
 
 
-def _flags(host: bool) -> int:
-    return _lib.FRAMING_HOST if host else 0
+def _flags(host) -> int:
+    """host=None: the library's size policy (nvl_framing_uses_gpu); True: the
+    host CRC; False: the GPU whatever the size."""
+    if host is None:
+        return 0
+    return _lib.FRAMING_HOST if host else _lib.FRAMING_GPU
 
 
 def _check(rc: int, what: str) -> None:
@@ -80,7 +86,7 @@ def _ro(data: BytesLike):
     return data, len(data), data
 
 
-def seal_trailers(image: Union[bytearray, np.ndarray], handles, *, host: bool = False) -> None:
+def seal_trailers(image: Union[bytearray, np.ndarray], handles, *, host: Optional[bool] = None) -> None:
     """TableBuilder::WriteRawBlock's trailer (table/table_builder.cc:183-188) for
     every (offset, size) handle, in place: image[off+size] holds the type,
     Mask(Value(block | type)) goes to image[off+size+1 .. +5)."""
@@ -94,7 +100,7 @@ def seal_trailers(image: Union[bytearray, np.ndarray], handles, *, host: bool = 
     _check(_lib.lib.nvl_sstable_seal_trailers(ptr, n, h.ctypes.data, len(h), _flags(host)), "seal_trailers")
 
 
-def verify_blocks(image: BytesLike, handles, *, host: bool = False) -> np.ndarray:
+def verify_blocks(image: BytesLike, handles, *, host: Optional[bool] = None) -> np.ndarray:
     """ReadBlock's checks (verify_checksums) for every handle: an array of
     NVL_BLOCK_* verdicts (see BLOCK_TEXT)."""
     h = _handles(handles)
@@ -137,7 +143,7 @@ class TableReport:
         return [b for b in self.blocks if b.verdict != _lib.BLOCK_OK]
 
 
-def verify_table(image: BytesLike, *, host: bool = False) -> TableReport:
+def verify_table(image: BytesLike, *, host: Optional[bool] = None) -> TableReport:
     """Every block of an SSTable image verified in one batch
     (nvl_sstable_verify_table): index, metaindex, meta blocks, data blocks."""
     ptr, n, _keep = _ro(image)
@@ -188,7 +194,7 @@ LOG_KIND = {_lib.LOG_RECORD: "record", _lib.LOG_BAD_LENGTH: "bad record length",
 
 
 def log_scan(image: BytesLike, *, start: int = 0, checksum: bool = True,
-             host: bool = False) -> List[Tuple[str, int, int, int]]:
+             host: Optional[bool] = None) -> List[Tuple[str, int, int, int]]:
     """ReadPhysicalRecord's outcomes over a log image (nvl_log_scan):
     [(kind, header_offset, payload_length, type)] ending with ("eof", ...)."""
     ptr, n, _keep = _ro(image)
@@ -207,7 +213,7 @@ def log_scan(image: BytesLike, *, start: int = 0, checksum: bool = True,
     return [(LOG_KIND[e.kind], e.offset, e.length, e.type) for e in ev[:cnt.value]]
 
 
-def log_seal(image: Union[bytearray, np.ndarray], header_offsets: Sequence[int], *, host: bool = False) -> None:
+def log_seal(image: Union[bytearray, np.ndarray], header_offsets: Sequence[int], *, host: Optional[bool] = None) -> None:
     """log::Writer's header CRCs (db/log_writer.cc:93-97) for every header offset, in place."""
     off = np.ascontiguousarray(np.asarray(header_offsets, dtype=np.uint64))
     if isinstance(image, np.ndarray):

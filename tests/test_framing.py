@@ -20,6 +20,7 @@ batch (marked gpu).
 import ctypes
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -29,6 +30,7 @@ from conftest import ROOT, gpu_present, load_golden
 
 NATIVE = os.path.join(ROOT, "tests", "native")
 HOST = 0x100
+GPU = 0x400  # NVL_FRAMING_GPU: force the GPU (flags = 0 picks by size)
 
 
 @pytest.fixture(scope="module")
@@ -123,7 +125,7 @@ def test_log_fixtures_host(shim, port):
 def test_log_fixtures_gpu(shim, port):
     if not gpu_present():
         pytest.skip("no GPU")
-    _check_log_fixtures(shim, port, 0)
+    _check_log_fixtures(shim, port, GPU)
 
 
 def _check_log_fixtures_streamed(shim, port, flags, windows):
@@ -154,7 +156,7 @@ def test_log_fixtures_streamed_host(shim, port):
 def test_log_fixtures_streamed_gpu(shim, port):
     if not gpu_present():
         pytest.skip("no GPU")
-    _check_log_fixtures_streamed(shim, port, 0, (1, 3, 17))
+    _check_log_fixtures_streamed(shim, port, GPU, (1, 3, 17))
 
 
 def test_log_stream_read_errors_vs_reference_live(shim, port):
@@ -322,7 +324,7 @@ def test_sstable_seal_verify_host(L, port):
 def test_sstable_seal_verify_gpu(L, port):
     if not gpu_present():
         pytest.skip("no GPU")
-    _check_sstable(L, port, 0)
+    _check_sstable(L, port, GPU)
 
 
 def test_sstable_trailers_golden(L):
@@ -338,12 +340,12 @@ def test_sstable_trailers_golden(L):
 def test_device_mode_fails_loudly_without_gpu(L):
     img = bytearray(b"abc" + bytes(5))
     h = np.array([[0, 3]], dtype=np.uint64)
-    assert _seal(L, img, h, 0) in (L.ENODEV, L.EHIP)
+    assert _seal(L, img, h, GPU) in (L.ENODEV, L.EHIP)
     assert img[-4:] == bytes(4)  # nothing written
     n = ctypes.c_size_t(0)
     log = bytes(7)
     log = b"\x01\x02\x03\x04\x01\x00\x01x"
-    assert L.lib.nvl_log_scan(log, len(log), 0, 1, None, 0, ctypes.byref(n), 0) in (L.ENODEV, L.EHIP)
+    assert L.lib.nvl_log_scan(log, len(log), 0, 1, None, 0, ctypes.byref(n), GPU) in (L.ENODEV, L.EHIP)
 
 
 def test_python_view_log(port):
@@ -366,3 +368,53 @@ def test_python_view_log(port):
     bad[hdrs[1] + 9] ^= 1
     ev = framing.log_scan(bytes(bad), host=True)
     assert [e[0] for e in ev] == ["record", "checksum mismatch", "eof"]
+
+
+def test_engine_policy(L):
+    """flags = 0 picks the engine by the checksummed bytes of a host-resident
+    call (the measured crossover, DESIGN §9); NVL_FRAMING_HOST / _GPU force one;
+    both at once is an argument error."""
+    lib = L.lib
+    m = lib.nvl_framing_gpu_min_bytes()
+    assert m > 0
+    for b in (0, 1, m - 1):
+        assert lib.nvl_framing_uses_gpu(b, 0) == 0
+    for b in (m, m + 1, 1 << 40):
+        assert lib.nvl_framing_uses_gpu(b, 0) == 1
+    for b in (0, 1 << 40):
+        assert lib.nvl_framing_uses_gpu(b, HOST) == 0
+        assert lib.nvl_framing_uses_gpu(b, GPU) == 1
+        assert lib.nvl_framing_uses_gpu(b, HOST | GPU) == L.EINVAL
+    img = bytearray(b"abc" + bytes(5))
+    h = np.array([[0, 3]], dtype=np.uint64)
+    assert _seal(L, img, h, HOST | GPU) == L.EINVAL and img[-4:] == bytes(4)
+
+
+def test_engine_policy_env_override():
+    code = ("import sys; sys.path.insert(0, %r); from nvlevelz_amd import _lib; "
+            "print(_lib.lib.nvl_framing_gpu_min_bytes(), _lib.lib.nvl_framing_uses_gpu(5000, 0), "
+            "_lib.lib.nvl_framing_uses_gpu(4999, 0))" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, NVL_FRAMING_GPU_MIN_BYTES="5000"))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["5000", "1", "0"]
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
+def test_engine_policy_without_gpu(L, port):
+    """No GPU: a small host-resident call takes the host CRC by policy and is
+    right; a call the policy sends to the GPU fails loudly (no fallback)."""
+    blocks = [port.fill(3 + k, 0, 1000).tobytes() for k in range(4)]
+    img, hs = bytearray(), []
+    for b in blocks:
+        hs.append((len(img), len(b)))
+        img += b + b"\0" + bytes(4)
+    h = np.array(hs, dtype=np.uint64)
+    assert _seal(L, img, h, 0) == L.OK
+    for (o, n) in hs:
+        assert int.from_bytes(img[o + n + 1:o + n + 5], "little") == port.mask(port.value(bytes(img[o:o + n + 1])))
+    m = L.lib.nvl_framing_gpu_min_bytes()
+    big = bytearray(m + 5)
+    hb = np.array([[0, m]], dtype=np.uint64)
+    assert _seal(L, big, hb, 0) in (L.ENODEV, L.EHIP)
+    assert big[-4:] == bytes(4)

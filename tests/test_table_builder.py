@@ -25,6 +25,7 @@ from conftest import gpu_present, load_golden
 from nvlevelz_amd import framing
 
 HOST = 0x100
+GPU = 0x400  # NVL_FRAMING_GPU
 
 
 def _cases(rng, count):
@@ -93,7 +94,7 @@ def test_tablefile_matches_reference_builder_gpu():
     rng = np.random.default_rng(1718)
     for keys, vals, bs, ri, bloom in _cases(rng, 20):
         ref, _ = rt.build(keys, vals, bs, ri, bloom)
-        img, _ = rt.build(keys, vals, bs, ri, bloom, via_shim=1, seal_flags=0)
+        img, _ = rt.build(keys, vals, bs, ri, bloom, via_shim=1, seal_flags=GPU)
         assert img == ref, (len(keys), bs, ri, bloom)
 
 
@@ -140,5 +141,5 @@ def test_deferred_crc_edit_gpu_seal():
     for keys, vals, bs, ri, bloom in _cases(rng, 10):
         ref, _ = stock.build(keys, vals, bs, ri, bloom)
         for mode in (1, 2):
-            img, _ = edited.build(keys, vals, bs, ri, bloom, via_shim=mode, seal_flags=0)
+            img, _ = edited.build(keys, vals, bs, ri, bloom, via_shim=mode, seal_flags=GPU)
             assert img == ref, (mode, len(keys), bs)

@@ -27,6 +27,7 @@ import table_cases as tc
 from conftest import ROOT, gpu_present, load_golden
 
 HOST = 0x100
+GPU = 0x400  # NVL_FRAMING_GPU: force the GPU (flags = 0 picks by size)
 NATIVE = os.path.join(ROOT, "tests", "native")
 
 
@@ -146,7 +147,7 @@ def test_table_reader_golden_host(harness, port):
 def test_table_reader_golden_gpu(harness, port):
     if not gpu_present():
         pytest.skip("no GPU")
-    _check_reader(harness, port, 0, every=30)
+    _check_reader(harness, port, GPU, every=30)
 
 
 def _check_golden(L, harness, port, flags):
@@ -170,7 +171,7 @@ def test_table_cases_golden_host(L, harness, port):
 def test_table_cases_golden_gpu(L, harness, port):
     if not gpu_present():
         pytest.skip("no GPU")
-    _check_golden(L, harness, port, 0)
+    _check_golden(L, harness, port, GPU)
 
 
 @pytest.mark.gpu
@@ -309,7 +310,7 @@ def test_table_verify_large_gpu(L, port):
     buf, handles, size = _big_table(port, nblocks, 4096)
     h = np.ascontiguousarray(handles)
     cbuf = (ctypes.c_char * len(buf)).from_buffer(buf)
-    assert L.lib.nvl_sstable_seal_trailers(cbuf, len(buf), h.ctypes.data, nblocks, 0) == 0
+    assert L.lib.nvl_sstable_seal_trailers(cbuf, len(buf), h.ctypes.data, nblocks, GPU) == 0
     del cbuf  # release the export so the image can grow
     data_end = len(buf)
     w = tc._Writer(port)
@@ -320,7 +321,7 @@ def test_table_verify_large_gpu(L, port):
     foot = tc.handle(*meta_h) + tc.handle(*index_h)
     w.img += foot + bytes(40 - len(foot)) + tc.MAGIC.to_bytes(8, "little")
     img = bytes(w.img)
-    st, blocks = verify(L, img, 0)
+    st, blocks = verify(L, img, GPU)
     assert st == 0 and len(blocks) == nblocks + 2
     assert all(b[3] == 0 for b in blocks)
     assert [b[:2] for b in blocks[2:]] == [(int(o), int(s)) for o, s in handles]
@@ -331,7 +332,7 @@ def test_table_verify_large_gpu(L, port):
         o = int(handles[k][0])
         mut[o + int(rng.integers(0, size))] ^= 1 << int(rng.integers(0, 8))
     assert data_end < len(mut)
-    st, blocks = verify(L, bytes(mut), 0)
+    st, blocks = verify(L, bytes(mut), GPU)
     assert st == 0
     assert [i for i, b in enumerate(blocks[2:]) if b[3]] == bad_idx
     assert all(blocks[2 + k][3] == L.BLOCK_CHECKSUM_MISMATCH for k in bad_idx)
@@ -376,4 +377,4 @@ def test_python_view_fails_loudly_without_gpu(port):
     from nvlevelz_amd import framing
     img, _ = tc.build(port, {"seed": 5, "nblocks": 3, "nmeta": 1})
     with pytest.raises(framing.FramingError):
-        framing.verify_table(img)
+        framing.verify_table(img, host=False)

@@ -18,6 +18,7 @@ ap.add_argument("--lib", default=None); ap.add_argument("--blocks", type=int, de
 ap.add_argument("--launches", type=int, default=20); ap.add_argument("--len", type=int, default=4096)
 ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "var4097", "gen", "rand", "varlen"])
 ap.add_argument("--gap", type=int, default=4)  # varlen: bytes between buffers
+ap.add_argument("--region", action="store_true", help="variable configs through nvl_crc32c_region_dev")
 a = ap.parse_args()
 lib = _lib.lib
 if a.lib:
@@ -59,6 +60,15 @@ else:
     o = torch.from_numpy(offs).to(dev)
     m = torch.from_numpy(lens).to(dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
+    if a.region:
+        wsb = lib.nvl_crc32c_region_workspace_bytes(total, n)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        for _ in range(a.launches):
+            assert lib.nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.data_ptr(), None, 0,
+                                             out.data_ptr(), n, 0, ws.data_ptr(), wsb, st) == 0
+        torch.cuda.synchronize()
+        print("done region", a.config, hex(int(out[0].item()) & 0xFFFFFFFF))
+        sys.exit(0)
     ws = torch.empty(lib.nvl_crc32c_batch_workspace_bytes(n), dtype=torch.uint8, device=dev)
     for _ in range(a.launches):
         assert lib.nvl_crc32c_batch_dev(buf.data_ptr(), o.data_ptr(), m.data_ptr(), None, 0, out.data_ptr(), n, 0,

@@ -380,6 +380,10 @@ int run_self_test(DeviceState* s) {
   return rc;
 }
 
+// Per-thread buffers above this size are released when a call needs less
+// than a quarter of them (DevSlab / table_pinned only grew).
+constexpr size_t kSlabKeep = 64u << 20;
+
 // Pinned host staging for the host-resident entry points (grown on demand,
 // one per thread so concurrent callers never share it).
 struct Staging {
@@ -391,7 +395,10 @@ struct Staging {
     host_bytes = 0;
   }
   void* get(size_t bytes) {
-    if (bytes > host_bytes) {
+    // grown on demand; a large buffer is given back when a call needs less
+    // than a quarter of it (a thread that once verified a huge table does
+    // not keep hundreds of MB pinned for good)
+    if (bytes > host_bytes || (host_bytes > kSlabKeep && bytes < host_bytes / 4)) {
       if (host) (void)hipHostFree(host);
       host = nullptr;
       host_bytes = 0;
@@ -452,7 +459,8 @@ struct DevSlab {
   }
   void* get(int dev, size_t bytes) {
     const uint64_t g = g_generation.load(std::memory_order_acquire);
-    if (dev == device && g == gen && bytes <= cap && p) return p;
+    // (shrunk like Staging: a huge slab goes when a call needs < 1/4 of it)
+    if (dev == device && g == gen && bytes <= cap && p && !(cap > kSlabKeep && bytes < cap / 4)) return p;
     int prev = -1;
     (void)hipGetDevice(&prev);
     if (device >= 0 && device != prev) (void)hipSetDevice(device);

@@ -1843,7 +1843,12 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
   }
   if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
   fill_lds<kWavesPerWG>(lds, ka.tables);
-  if (!fused_scan) __syncthreads();
+  // Every path passes this barrier before its first table lookup and its
+  // first list append: it orders the LDS fill AND wave 0's zeroing of the
+  // list counters ctl before them (round 3 faulted a parity test,
+  // test_varlen_plan_paths[32769], when an append could land before the
+  // zeroing; the fused path's scan barrier below no longer carries that).
+  __syncthreads();
   NVL_TL(2);
   if (fused_scan) {  // (the first -- and only -- sub-range's lanes hold their metadata)
     uint64_t gb, ge;
@@ -1864,11 +1869,7 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
       for (int o = 32; o > 0; o >>= 1) mj = max(mj, (uint32_t)__shfl_xor((int)mj, o));
       if (lane == 63) wsum[wv] = x;
       if (lane == 0) wmax[wv] = mj;
-      // (also: the tables are in LDS, and wave 0's zeroing of the list
-      // counters ctl is ordered before every wave's list appends -- without
-      // this barrier an append could land first: round 3 faulted a parity
-      // test that way)
-      __syncthreads();
+      __syncthreads();  // wsum / wmax complete
       // the 16 waves' totals and flags across lanes 0..15 (a wave scan, not
       // 48 LDS reads held in registers at once)
       const bool lw = (uint32_t)lane < kWavesPerWG;
@@ -2089,23 +2090,25 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
 #ifndef NVL_GEN_PAIR_U
 #define NVL_GEN_PAIR_U 2  // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 91.7 through run_units)
 #endif
-#if !defined(NVL_GEN_NO_PAIRS)
   if constexpr (M == kGeneral) {
+#if !defined(NVL_GEN_NO_PAIRS)
     // one whole chunk per buffer (len == 4096, any alignment): scheduler A,
     // one buffer per unit, no records
     if (g.J == 1 && !head_first(g.len)) {
       run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
       return;
     }
+#endif
     // one partial chunk per buffer, 1025..4095 bytes (launch_fixed): each
     // buffer a long head, in scheduler A's order (10^5 x 3500 B at stride
-    // 4128: 75.3 -> 71.3 us against the head kernel, profiles/r03_ablations)
+    // 4128: 75.3 -> 71.3 us against the head kernel, profiles/r03_ablations).
+    // Outside the variant switch above: launch_fixed sends these batches here
+    // without a head kernel, so no build may drop this path.
     if (g.J == 1) {
       run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kMasked>(g, ka, lds);
       return;
     }
   }
-#endif
   if constexpr (M == kGeneral) run_general<waves_of<M>()>(g, ka, lds);
   else run_units<M, waves_of<M>()>(g, ka, lds);
 }
@@ -3319,8 +3322,11 @@ static inline size_t recs_part(int num_cu, uint64_t len, uint64_t n) {
 // Fixed-stride workspace: [unit records (J > 1)][hc: n u32 (partial first chunks with J > 1)]
 // or, for a shape that can take the chunk-parallel path (len a multiple of
 // 4096, J > 1: aligned when base and stride are), the n*J chunk raws if larger.
+constexpr uint32_t kChunkParallelMaxJ = 1024;  // fold runs of <= 16 raws per lane (config 4: J = 512, R = 8)
+
 static inline size_t chunk_raws_bytes(uint64_t len, uint64_t n) {
-  return (len > dev::kChunk && len % dev::kChunk == 0) ? n * (len / dev::kChunk) * sizeof(uint32_t) : 0;
+  return (len > dev::kChunk && len % dev::kChunk == 0 && len / dev::kChunk <= kChunkParallelMaxJ)
+             ? n * (len / dev::kChunk) * sizeof(uint32_t) : 0;
 }
 size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
   const size_t cr = chunk_raws_bytes(len, n);
@@ -3356,7 +3362,12 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
     if (eh != hipSuccess || !body) return eh;
     ev_start = nullptr;
   }
-  if (aligned && J > 1) {  // chunk-parallel: every chunk a scheduler-A pass, then the per-buffer fold
+  // Chunk-parallel (every chunk a scheduler-A pass, then the per-buffer fold)
+  // while a fold lane's serial run R = ceil(J/64) stays short: the fold is one
+  // wave per buffer, so a few huge buffers (n = 1 x 1 GiB: R = 4096) would
+  // fold for longer than they stream; those take scheduler B, whose units
+  // split the chunk space over the whole grid (bench_configs `big1`).
+  if (aligned && J > 1 && J <= kChunkParallelMaxJ) {
     const uint64_t T = n * (uint64_t)J;
     const uint32_t jsh = (J & (J - 1u)) == 0u ? (uint32_t)__builtin_ctz(J) : 64u;
     dev::ChunkGeom cg{base, stride, T, J, jsh, init, init_all};

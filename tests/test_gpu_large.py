@@ -100,3 +100,21 @@ def test_fixed_general_giant(dev, C, port, L, n, stride_gap, base_off):
     got = _u32(C.extend_fixed(buf[base_off:], stride, L, n, torch.from_numpy(inits.view(np.int32)).to(dev)))
     want = port.fixed(host[base_off:], stride, L, n, inits)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("J,n", [(1025, 3), (262144, 1), (4096, 2)])
+def test_fixed_aligned_long_buffers(dev, C, port, J, n):
+    """Aligned fixed-stride batches of buffers longer than the chunk-parallel
+    fold takes (J > 1024 chunks: scheduler B, unit records, fix-up), incl. a
+    lone 1 GiB buffer, with per-buffer inits and Mask."""
+    L = J * 4096
+    host = port.fill(0xA1A + J, 0, n * L)
+    buf = torch.from_numpy(host).to(dev)
+    rng = np.random.default_rng(J)
+    inits = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    got = _u32(C.extend_fixed(buf, L, L, n, torch.from_numpy(inits.view(np.int32)).to(dev)))
+    want = port.fixed(host, L, L, n, inits)
+    assert np.array_equal(got, want)
+    gotm = _u32(C.extend_fixed(buf, L, L, n, mask=True))
+    want0 = port.fixed(host, L, L, n)
+    assert [int(x) for x in gotm] == [port.mask(int(x)) for x in want0]

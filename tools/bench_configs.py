@@ -3,6 +3,7 @@ around each call, median of R reps), every result checked.
     python tools/bench_configs.py [--lib build/libnvl_crc32c_X.so] [--configs 2,3,4,v,g,r]
   2, 3, 4  BASELINE configs 2-4 (golden digests)
   3R, vR, rR  config 3, v and r through nvl_crc32c_region_dev (the region path)
+  big1     one aligned 1 GiB buffer (fixed path, n = 1)
   v        10^5 x 4097 B at stride 4101: block | type of 4096-byte SSTable blocks with their
            4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
   g        10^5 x 4096 B at stride 4099 from an odd base: the fixed-stride general path
@@ -75,6 +76,17 @@ for c in a.configs.split(","):
         fn = lambda: lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, out.data_ptr(), 0, ws.data_ptr(), wsb, st)
         alg = n * (L + 4)
         check = lambda res: p.digest(res) == cfg["digest"]
+    elif c == "big1":  # one aligned 1 GiB buffer (a lone huge fixed batch: scheduler B, not the chunk fold)
+        n, L = 1, 1 << 30
+        buf = torch.empty(L, dtype=torch.uint8, device=dev)
+        lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), L // 8, 8, 0, 1, 0x5EED0B16, None)
+        out = torch.empty(1, dtype=torch.int32, device=dev)
+        wsb = max(1, lib.nvl_crc32c_fixed_workspace_bytes(L, L, 1))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fn = lambda: lib.nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, 1, None, 0, out.data_ptr(), 0, ws.data_ptr(), wsb, st)
+        alg = L + 4
+        want = p.fixed(buf.cpu().numpy(), L, L, 1)
+        check = lambda res: bool(np.array_equal(res, want))
     elif c in ("3", "3R"):
         cfg = g["cfg3"]; total = cfg["total"]
         lens = p.cfg3_lengths(cfg["len_seed"], total)

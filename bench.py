@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--shims", action="store_true",
                     help="also time the whole-table verify shim on a host-resident 10^5-block SSTable image")
     ap.add_argument("--verify", action="store_true", default=True)
+    ap.add_argument("--sustained", type=int, default=2000,
+                    help="untimed back-to-back launches after the timed region (segment periods; 0 = skip)")
     return ap.parse_args()
 
 
@@ -466,6 +468,23 @@ def main():
         iso[2 * k + 1].record(stream)
     torch.cuda.synchronize()
     iso_ms = [iso[2 * k].elapsed_time(iso[2 * k + 1]) for k in range(K)]
+    #  * sustained: --sustained back-to-back launches (default 2000, ~0.13 s)
+    #    with an event every 100, so drift from the short timed window to a
+    #    long run shows as a series of segment periods
+    sus = None
+    if args.sustained > 0:
+        seg = 100
+        nseg = max(1, args.sustained // seg)
+        sev = [torch.cuda.Event(enable_timing=True) for _ in range(nseg + 1)]
+        sev[0].record(stream)
+        for j in range(nseg):
+            for _ in range(seg):
+                step()
+            sev[j + 1].record(stream)
+        torch.cuda.synchronize()
+        segs = [sev[j].elapsed_time(sev[j + 1]) * 1e3 / seg for j in range(nseg)]
+        sus = {"launches": nseg * seg, "segment_launches": seg,
+               "segment_period_us": [round(x, 2) for x in segs]}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -567,6 +586,16 @@ def main():
             "cpu_baseline": cpu,
             "verify": verify,
         }
+        if sus:
+            mp = float(np.mean(sus["segment_period_us"]))
+            sus.update({"mean_period_us": round(mp, 2), "frac": round(alg_bytes / (mp * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                        "first_segment_frac": round(alg_bytes / (sus["segment_period_us"][0] * 1e-6) / 1e9 /
+                                                    HBM_PEAK_GBS, 4),
+                        "last_segment_frac": round(alg_bytes / (sus["segment_period_us"][-1] * 1e-6) / 1e9 /
+                                                   HBM_PEAK_GBS, 4),
+                        "what": "untimed diagnostic after the timed region: back-to-back launches, HIP events every "
+                                "100; frac over the whole run (the timed window's frac is roofline.frac)"})
+            line["roofline"]["sustained"] = sus
         if e2e:
             line["e2e"] = e2e
         if args.shims and N == 1:

@@ -3047,7 +3047,13 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
         row_transpose(wd[k]);
       }
-      chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf);
+      if (em.ms | em.me) {
+        chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf);
+      } else {  // no buffer starts or ends inside these chunks (most of config 3's units)
+        chains_keep<U>(lds, lb, wd, lane, lr, raw);
+#pragma unroll
+        for (int k = 0; k < U; ++k) qf[k] = 0u;
+      }
     } else {  // the range's single-chunk units
       uint32_t wd[1][16], l1[1], r1[1], f1[1] = {Lf[0]}, q1[1];
 #pragma unroll

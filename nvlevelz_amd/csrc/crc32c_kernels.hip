@@ -3017,8 +3017,30 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   load_unit(ca, cu, cur);
   uint64_t cursor = cu ? region_search(g, ca * kChunk, lane) : g.n;
   WinRaw wr = load_win(g, cursor, lane);
+  // The batch check (sorted by offset, non-overlapping, inside the region),
+  // one slice per wave: the first 64 buffers' loads go out before the LDS
+  // fill so their latency hides behind it (a check after the units delayed
+  // the last wave's end).
+  const uint64_t per = (g.n + (uint64_t)gridDim.x * kWavesPerWG - 1u) / ((uint64_t)gridDim.x * kWavesPerWG);
+  const uint64_t i0 = min(g.n, ((uint64_t)blockIdx.x * kWavesPerWG + wv) * per), i1 = min(g.n, i0 + per);
+  const uint64_t ci = min(i0 + (uint64_t)lane, g.n - 1u), cp = ci ? ci - 1u : 0u;
+  const uint64_t co = ldg64(g.offsets, ci), cl = ldg64(g.lengths, ci);
+  const uint64_t po = ldg64(g.offsets, cp), pl = ldg64(g.lengths, cp);
   fill_lds<kWavesPerWG>(lds, ka.tables);
   __syncthreads();
+  {
+    bool bad = false;
+    if (i0 + (uint64_t)lane < i1) {
+      bad = co > g.region_len || cl > g.region_len - co;
+      if (ci > 0) bad |= co < po + pl;
+    }
+    for (uint64_t i = i0 + 64u + (uint64_t)lane; i < i1; i += 64u) {  // slices of more than 64 buffers
+      const uint64_t o = ldg64(g.offsets, i), L = ldg64(g.lengths, i);
+      bad |= o > g.region_len || L > g.region_len - o;
+      bad |= o < ldg64(g.offsets, i - 1) + ldg64(g.lengths, i - 1);
+    }
+    if (__ballot(bad) && lane == 0) g.ctr[kRegionFlag] = 1u;
+  }
   const LaneBase lb = make_lane_base(lane);
 
   while (u < nunits) {
@@ -3083,17 +3105,6 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     for (int k = 0; k < U; ++k) cur[k] = nxt[k];
   }
 
-  // The batch check, one slice per wave (after its units: the waves end
-  // apart anyway): sorted by offset, non-overlapping, inside the region.
-  const uint64_t per = (g.n + (uint64_t)gridDim.x * kWavesPerWG - 1u) / ((uint64_t)gridDim.x * kWavesPerWG);
-  const uint64_t i0 = min(g.n, ((uint64_t)blockIdx.x * kWavesPerWG + wv) * per), i1 = min(g.n, i0 + per);
-  bool bad = false;
-  for (uint64_t i = i0 + (uint64_t)lane; i < i1; i += 64u) {
-    const uint64_t o = ldg64(g.offsets, i), L = ldg64(g.lengths, i);
-    bad |= o > g.region_len || L > g.region_len - o;
-    if (i > 0) bad |= o < ldg64(g.offsets, i - 1) + ldg64(g.lengths, i - 1);
-  }
-  if (__ballot(bad) && lane == 0) g.ctr[kRegionFlag] = 1u;
 }
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {

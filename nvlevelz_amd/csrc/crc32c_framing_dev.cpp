@@ -160,10 +160,13 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   if (2 + nr > cap) return NVL_CRC32C_OK;                     // the generic walk reports ENOSPC
 
   // 2. device workspace: [results][boff][blen][crc][vk][records][batch workspace]
-  const uint64_t nmax = nr + np + nm_max;
+  //    Slots in file order: data [0, nr), meta + zero-length fillers [nr, pb),
+  //    index pieces [pb, pb + np): one region batch over the image.
+  const uint64_t pb = nr + nm_max, nmax = pb + np;
+  if (nmax > 0xFFFFFFFFull) return NVL_CRC32C_OK;
   const size_t s_res = up256(kResHead + 4 * np + nm_max), s8 = up256(nmax * 8), s4 = up256(nmax * 4),
                s1 = up256(nmax), s_rec = up256(nr * sizeof(nvl_table_block));
-  const size_t wsb = nvl_crc32c_batch_workspace_bytes(nmax);
+  const size_t wsb = nvl_crc32c_region_workspace_bytes(len, nmax);
   uint8_t* d = static_cast<uint8_t*>(thread_table_device(dev, s_res + 2 * s8 + s4 + s1 + s_rec + wsb));
   if (!d) return NVL_CRC32C_EHIP;
   uint8_t* dres = d;
@@ -173,7 +176,7 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   uint8_t* vk = d + s_res + 2 * s8 + s4;
   nvl_table_block* rec = reinterpret_cast<nvl_table_block*>(d + s_res + 2 * s8 + s4 + s1);
   void* ws = d + s_res + 2 * s8 + s4 + s1 + s_rec;
-  // pinned: [metaindex][meta slots: off, len1 | vk][results]
+  // pinned: [metaindex][meta + filler slots: off, len1 | vk][results]
   const size_t p_meta = 0, p_slots = up256(kMetaMax), p_res = p_slots + up256(nm_max * 17);
   pin = static_cast<uint8_t*>(thread_table_pinned(p_res + s_res));
   if (!pin) return NVL_CRC32C_EHIP;
@@ -185,8 +188,8 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
                                 hipMemcpyDeviceToHost, st) != hipSuccess)
     return NVL_CRC32C_EHIP;
   if (hipEventRecord(ev_meta, st) != hipSuccess ||
-      launch_index_entries(f, len, index_h.offset, index_h.size, (uint32_t)nr, (uint32_t)np, boff, blen, vk, rec,
-                           reinterpret_cast<uint32_t*>(dres), st) != hipSuccess ||
+      launch_index_entries(f, len, index_h.offset, index_h.size, (uint32_t)nr, (uint32_t)np, (uint32_t)pb, boff, blen,
+                           vk, rec, reinterpret_cast<uint32_t*>(dres), st) != hipSuccess ||
       hipEventRecord(ev_parse, st) != hipSuccess || hipEventSynchronize(ev_meta) != hipSuccess)
     return NVL_CRC32C_EHIP;
   uint8_t v_meta = NVL_BLOCK_TRUNCATED;
@@ -197,32 +200,47 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
     v_meta = host_block_verdict(mb, meta_h.size);
     if (v_meta == NVL_BLOCK_OK && mb[meta_h.size] == 0) block_handles(mb, meta_h.size, &meta_blocks, &meta_bad);
   }
-  const uint64_t nm = meta_blocks.size(), n = nr + np + nm, cnt = 2 + nm + nr;
+  const uint64_t nm = meta_blocks.size(), n = nmax, cnt = 2 + nm + nr;
   if (nm > nm_max || cnt > cap) {  // (nm_max bounds it) / the generic walk reports ENOSPC
     (void)hipStreamSynchronize(st);
     return NVL_CRC32C_OK;
   }
 
-  // 4. meta slots, then ONE batch over data blocks + index pieces + meta blocks
+  // 4. meta slots and fillers [nr, pb), then ONE region batch over data
+  //    blocks + meta blocks + index pieces.  A zero-length filler sits at the
+  //    index block's offset (between the meta blocks and the first piece, so
+  //    the slots stay in file order); a meta slot that is not read gets length
+  //    0 at the previous slot's end for the same reason.  (A table whose
+  //    blocks are out of file order still verifies: the region path then
+  //    checksums the batch serially, correct and slow.)
+  const uint64_t nf = nm_max;
   uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
-  uint8_t* mv = pin + p_slots + nm * 16;
-  for (uint64_t j = 0; j < nm; ++j) {
-    const nvl_block_handle& b = meta_blocks[j];
-    const bool fits = !meta_bad[j] && block_in_file(b, len);
-    ms[j] = b.offset;
-    ms[nm + j] = fits ? b.size + 1 : 0;
-    mv[j] = meta_bad[j] ? (uint8_t)NVL_BLOCK_BAD_HANDLE : (fits ? kCompute : (uint8_t)NVL_BLOCK_TRUNCATED);
+  uint8_t* mv = pin + p_slots + nf * 16;
+  uint64_t prev_end = 0;
+  for (uint64_t j = 0; j < nf; ++j) {
+    if (j < nm) {
+      const nvl_block_handle& b = meta_blocks[j];
+      const bool fits = !meta_bad[j] && block_in_file(b, len);
+      ms[j] = fits ? b.offset : prev_end;
+      ms[nf + j] = fits ? b.size + 1 : 0;
+      mv[j] = meta_bad[j] ? (uint8_t)NVL_BLOCK_BAD_HANDLE : (fits ? kCompute : (uint8_t)NVL_BLOCK_TRUNCATED);
+      if (fits) prev_end = b.offset + b.size + 1;
+    } else {
+      ms[j] = index_h.offset;
+      ms[nf + j] = 0;
+      mv[j] = (uint8_t)NVL_BLOCK_OK;  // no verdict of its own
+    }
   }
-  const uint64_t m0 = nr + np;
-  if (nm && (hipMemcpyAsync(boff + m0, ms, nm * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-             hipMemcpyAsync(blen + m0, ms + nm, nm * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-             hipMemcpyAsync(vk + m0, mv, nm, hipMemcpyHostToDevice, st) != hipSuccess))
+  if (nf && (hipMemcpyAsync(boff + nr, ms, nf * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+             hipMemcpyAsync(blen + nr, ms + nf, nf * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+             hipMemcpyAsync(vk + nr, mv, nf, hipMemcpyHostToDevice, st) != hipSuccess))
     return NVL_CRC32C_EHIP;
-  int rc = nvl_crc32c_batch_dev(f, boff, blen, nullptr, 0, crc, n, 0, ws, nvl_crc32c_batch_workspace_bytes(n), st);
+  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, n, 0, ws, wsb, st);
   if (rc != NVL_CRC32C_OK) return rc;
   const size_t res_bytes = kResHead + 4 * np + nm;
   uint8_t* res = pin + p_res;
-  if (launch_table_verdicts(f, boff, blen, crc, n, (uint32_t)nr, (uint32_t)np, vk, dres, st) != hipSuccess ||
+  if (launch_table_verdicts(f, boff, blen, crc, n, (uint32_t)nr, (uint32_t)nm, (uint32_t)pb, (uint32_t)np, vk,
+                            dres, st) != hipSuccess ||
       hipMemcpyAsync(res, dres, res_bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
     return NVL_CRC32C_EHIP;
   // the records, on the side stream once the parse has written them

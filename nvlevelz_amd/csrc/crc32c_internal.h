@@ -107,14 +107,17 @@ hipError_t launch_trailer_verdicts(const void* file, const uint64_t* off, const 
 // nvl_sstable_verify_table_dev's fast path (crc32c_table_dev.hip): batch
 // slots [0, nr) from the entries of a restart-interval-1 index block, parsed
 // one per thread (records rec[i]; *bad |= 1 when the block is not in the form
-// the sequential walk reads the same way), [nr, nr + np) the index block in
-// 4096-byte pieces; then ReadBlock's trailer checks for every slot whose
-// verdict vk[k] is still 0xFF, with counts, piece CRCs and meta verdicts in res.
+// the sequential walk reads the same way), [nr, nr + nm) the meta blocks
+// (host), up to pb zero-length fillers, [pb, pb + np) the index block in
+// 4096-byte pieces -- file order; then ReadBlock's trailer checks for every
+// slot whose verdict vk[k] is still 0xFF, with counts, piece CRCs and meta
+// verdicts in res.
 hipError_t launch_index_entries(const void* file, uint64_t file_len, uint64_t index_off, uint64_t size, uint32_t nr,
-                                uint32_t np, uint64_t* boff, uint64_t* blen, uint8_t* vk, nvl_table_block* rec,
-                                uint32_t* bad, hipStream_t st);
+                                uint32_t np, uint32_t pb, uint64_t* boff, uint64_t* blen, uint8_t* vk,
+                                nvl_table_block* rec, uint32_t* bad, hipStream_t st);
 hipError_t launch_table_verdicts(const void* file, const uint64_t* boff, const uint64_t* blen, const uint32_t* crc,
-                                 uint64_t n, uint32_t nr, uint32_t np, uint8_t* vk, void* res, hipStream_t st);
+                                 uint64_t n, uint32_t nr, uint32_t nm, uint32_t pb, uint32_t np, uint8_t* vk,
+                                 void* res, hipStream_t st);
 // Its per-thread resources (crc32c_capi.cpp): device memory on `device`,
 // pinned host memory (both grown on demand, reused by the thread's next
 // call), a second stream and two events on `device`.

@@ -3136,11 +3136,19 @@ __device__ __forceinline__ uint32_t fold_step1(const uint32_t* t, uint32_t crc, 
   return t[(crc ^ b) & 255u] ^ (crc >> 8);
 }
 
-// raw(s, [p, p + L)) serially: bytes to a 4-byte boundary, STEP4 words, bytes.
+// raw(s, [p, p + L)) serially: bytes to a 4-byte boundary, STEP4 words (32
+// bytes' loads in flight at a time), bytes.
 __device__ uint32_t serial_raw(const uint32_t* t, uint32_t crc, const uint8_t* p, uint64_t L) {
   while (L && ((uintptr_t)p & 3u)) {
     crc = fold_step1(t, crc, *p++);
     --L;
+  }
+  for (; L >= 32; L -= 32, p += 32) {
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = reinterpret_cast<const uint32_t*>(p)[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) crc = fold_slice4(t, crc ^ w[k]);
   }
   for (; L >= 4; L -= 4, p += 4) crc = fold_slice4(t, crc ^ *reinterpret_cast<const uint32_t*>(p));
   while (L--) crc = fold_step1(t, crc, *p++);

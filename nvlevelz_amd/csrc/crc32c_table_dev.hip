@@ -55,28 +55,33 @@ constexpr uint64_t kResHead = 32;    // res: u32 bad, pad, u64 n_bad, u64 n_fix,
 
 }  // namespace
 
-// Batch slots: [0, nr) the data blocks the index entries point at, [nr,
-// nr + np) the index block itself in np pieces of 4096 bytes (the last one
-// shorter; their CRCs are combined on the host), then the meta blocks (the
-// host writes those).  Thread i < nr parses entry i of the index block [blk,
-// blk + size) with nr restart points -> slot i (offset, size + 1: block |
-// type; length 0 with a verdict preset when the handle is bad or out of the
-// file) and output record rec[i] = {offset, size, NVL_TBLOCK_DATA, preset or
-// OK}; *bad |= 1 when the entry is not where the sequential walk would find
-// it.  Thread nr + k writes piece slot k.
+// Batch slots, in file order (TableBuilder writes data blocks, meta blocks,
+// the metaindex, the index: table_builder.cc:241-266) so that the batch runs
+// as one region (nvl_crc32c_region_dev): [0, nr) the data blocks the index
+// entries point at, [nr, pb) the meta blocks and zero-length fillers (the
+// host writes those), [pb, pb + np) the index block itself in np pieces of
+// 4096 bytes (the last one shorter; their CRCs are combined on the host).
+// Thread i < nr parses entry i of the index block [blk, blk + size) with nr
+// restart points -> slot i (offset, size + 1: block | type; length 0 with a
+// verdict preset when the handle is bad or out of the file) and output record
+// rec[i] = {offset, size, NVL_TBLOCK_DATA, preset or OK}; *bad |= 1 when the
+// entry is not where the sequential walk would find it.  Thread nr + k writes
+// piece slot pb + k.
 __global__ void crc32c_index_entries(const uint8_t* __restrict__ file, uint64_t file_len, uint64_t index_off,
-                                     uint64_t size, uint32_t nr, uint32_t np, uint64_t* __restrict__ boff,
-                                     uint64_t* __restrict__ blen, uint8_t* __restrict__ vk,
-                                     nvl_table_block* __restrict__ rec, uint32_t* __restrict__ bad) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (uint64_t)nr + np) return;
-  if (i >= nr) {
-    const uint64_t k = i - nr, o = k * kPiece, ilen = size + 1;
+                                     uint64_t size, uint32_t nr, uint32_t np, uint32_t pb,
+                                     uint64_t* __restrict__ boff, uint64_t* __restrict__ blen,
+                                     uint8_t* __restrict__ vk, nvl_table_block* __restrict__ rec,
+                                     uint32_t* __restrict__ bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint64_t)nr + np) return;
+  if (t >= nr) {
+    const uint64_t k = t - nr, o = k * kPiece, ilen = size + 1, i = pb + k;
     boff[i] = index_off + o;
     blen[i] = ilen - o < kPiece ? ilen - o : kPiece;
     vk[i] = (uint8_t)NVL_BLOCK_OK;  // no verdict of its own
     return;
   }
+  const uint64_t i = t;
   const uint8_t* blk = file + index_off;
   const uint64_t restarts = size - (1ull + nr) * 4ull;
   const uint8_t* limit = blk + restarts;
@@ -124,12 +129,12 @@ __global__ void crc32c_index_entries(const uint8_t* __restrict__ file, uint64_t 
 // be computed (vk == kCompute): the trailer's type byte at off + len1 - 1,
 // its masked CRC after.  Results for the host in res: res64[1] = slots not
 // OK, res64[2] = data slots (k < nr) whose checked verdict is not the OK
-// their record was given, then the np piece CRCs (u32) and the meta slots'
-// verdicts (u8).
+// their record was given, then the np piece CRCs (u32, slots [pb, pb + np))
+// and the nm meta slots' verdicts (u8, slots [nr, nr + nm)).
 __global__ void crc32c_table_verdicts(const uint8_t* __restrict__ file, const uint64_t* __restrict__ boff,
                                       const uint64_t* __restrict__ blen, const uint32_t* __restrict__ crc,
-                                      uint64_t n, uint32_t nr, uint32_t np, uint8_t* __restrict__ vk,
-                                      uint8_t* __restrict__ res) {
+                                      uint64_t n, uint32_t nr, uint32_t nm, uint32_t pb, uint32_t np,
+                                      uint8_t* __restrict__ vk, uint8_t* __restrict__ res) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   uint8_t v = vk[k];
@@ -141,8 +146,8 @@ __global__ void crc32c_table_verdicts(const uint8_t* __restrict__ file, const ui
                                       : (t[0] > 1u ? (uint8_t)NVL_BLOCK_BAD_TYPE : (uint8_t)NVL_BLOCK_OK);
     vk[k] = v;
   }
-  if (k >= nr && k < (uint64_t)nr + np) reinterpret_cast<uint32_t*>(res + kResHead)[k - nr] = crc[k];
-  if (k >= (uint64_t)nr + np) res[kResHead + 4ull * np + (k - nr - np)] = v;
+  if (k >= pb && k < (uint64_t)pb + np) reinterpret_cast<uint32_t*>(res + kResHead)[k - pb] = crc[k];
+  if (k >= nr && k < (uint64_t)nr + nm) res[kResHead + 4ull * np + (k - nr)] = v;
   unsigned long long* c = reinterpret_cast<unsigned long long*>(res);
   const unsigned long long mb = __ballot(v != NVL_BLOCK_OK);
   const unsigned long long mf = __ballot(computed && k < nr && v != NVL_BLOCK_OK);
@@ -154,20 +159,23 @@ __global__ void crc32c_table_verdicts(const uint8_t* __restrict__ file, const ui
 }  // namespace dev
 
 hipError_t launch_index_entries(const void* file, uint64_t file_len, uint64_t index_off, uint64_t size, uint32_t nr,
-                                uint32_t np, uint64_t* boff, uint64_t* blen, uint8_t* vk, nvl_table_block* rec,
-                                uint32_t* bad, hipStream_t st) {
+                                uint32_t np, uint32_t pb, uint64_t* boff, uint64_t* blen, uint8_t* vk,
+                                nvl_table_block* rec, uint32_t* bad, hipStream_t st) {
   const uint64_t threads = (uint64_t)nr + np;
   if (threads == 0) return hipSuccess;
   hipLaunchKernelGGL(dev::crc32c_index_entries, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, st,
-                     static_cast<const uint8_t*>(file), file_len, index_off, size, nr, np, boff, blen, vk, rec, bad);
+                     static_cast<const uint8_t*>(file), file_len, index_off, size, nr, np, pb, boff, blen, vk, rec,
+                     bad);
   return hipGetLastError();
 }
 
 hipError_t launch_table_verdicts(const void* file, const uint64_t* boff, const uint64_t* blen, const uint32_t* crc,
-                                 uint64_t n, uint32_t nr, uint32_t np, uint8_t* vk, void* res, hipStream_t st) {
+                                 uint64_t n, uint32_t nr, uint32_t nm, uint32_t pb, uint32_t np, uint8_t* vk,
+                                 void* res, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(dev::crc32c_table_verdicts, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
-                     static_cast<const uint8_t*>(file), boff, blen, crc, n, nr, np, vk, static_cast<uint8_t*>(res));
+                     static_cast<const uint8_t*>(file), boff, blen, crc, n, nr, nm, pb, np, vk,
+                     static_cast<uint8_t*>(res));
   return hipGetLastError();
 }
 

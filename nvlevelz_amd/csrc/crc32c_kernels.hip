@@ -2740,8 +2740,8 @@ struct RegionGeom {
   const uint64_t* lengths;
   uint64_t n;
   uint32_t* raws;  // [nc]
-  uint32_t* qs;    // [n] Qe of buffer i's start event
-  uint32_t* qe;    // [n] Qe of its end event
+  uint2* qs;       // [n] buffer i's start event: {Qe, lane L's chain checkpoint x_4c}
+  uint2* qe;       // [n] its end event
   uint32_t* ctr;   // the stream's counter block
 };
 
@@ -2816,9 +2816,13 @@ __device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane) {
 
 // Chains and butterflies of U chunks, keeping each lane's piece raw (the
 // input of the events' masked butterflies).
+// cp[u][c - 1] = the chain register before word 4c (c = 1, 2, 3): the state
+// after 4c words with word 4c XORed in (x_4c = S_4c ^ w[4c]); an event's
+// record carries its lane's checkpoint, so the fold kernel re-runs at most 3
+// words of the piece instead of 15.
 template <int U>
 __device__ __forceinline__ void chains_keep(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
-                                            int lane, uint32_t (&lr)[U], uint32_t (&raw)[U]) {
+                                            int lane, uint32_t (&lr)[U], uint32_t (&raw)[U], uint32_t (&cp)[U][3]) {
   uint32_t crc[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) crc[u] = w[u][0];
@@ -2826,6 +2830,10 @@ __device__ __forceinline__ void chains_keep(const uint8_t* lds, const LaneBase& 
   for (int k = 0; k < 16; ++k) {
 #pragma unroll
     for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+    if (k == 3 || k == 7 || k == 11) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) cp[u][k >> 2] = crc[u];
+    }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) lr[u] = crc[u];
@@ -2852,7 +2860,7 @@ __device__ __forceinline__ void chains_keep(const uint8_t* lds, const LaneBase& 
 template <int U>
 __device__ __forceinline__ void chains_first(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
                                              int lane, const uint32_t (&Lf)[U], uint32_t (&lr)[U],
-                                             uint32_t (&raw)[U], uint32_t (&qf)[U]) {
+                                             uint32_t (&raw)[U], uint32_t (&qf)[U], uint32_t (&cp)[U][3]) {
   uint32_t crc[2 * U];
 #pragma unroll
   for (int u = 0; u < U; ++u) crc[u] = w[u][0];
@@ -2860,6 +2868,10 @@ __device__ __forceinline__ void chains_first(const uint8_t* lds, const LaneBase&
   for (int k = 0; k < 16; ++k) {
 #pragma unroll
     for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+    if (k == 3 || k == 7 || k == 11) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) cp[u][k >> 2] = crc[u];
+    }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -2916,8 +2928,8 @@ __device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr,
 template <int U>
 __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t* lds, Win w, uint64_t cur,
                                               uint64_t ca, uint32_t cu, const uint32_t (&lr)[U],
-                                              const uint32_t (&Lf)[U], const uint32_t (&qf)[U], EvMasks em,
-                                              int lane) {
+                                              const uint32_t (&Lf)[U], const uint32_t (&qf)[U],
+                                              const uint32_t (&cp)[U][3], EvMasks em, int lane) {
   const uint64_t A = ca * kChunk, B = (ca + cu) * kChunk;
   uint32_t pk = ~0u, pL = ~0u, pq = 0;
   for (;;) {
@@ -2943,7 +2955,15 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t
           pk = k;
           pL = L;
         }
-        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = pq;
+        // lane L's checkpoint before word 4c of its piece (c = 0: the zero state)
+        const uint32_t c = (pos >> 4) & 3u;
+        uint32_t x = 0u;
+#pragma unroll
+        for (int q = 0; q < U; ++q)
+#pragma unroll
+          for (int m = 0; m < 3; ++m) x = (k == (uint32_t)q && c == (uint32_t)m + 1u) ? cp[q][m] : x;
+        const uint32_t xl = lane_u32(x, L);
+        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = make_uint2(pq, c ? xl : 0u);
       }
     }
     if (cur + 64u >= g.n || lane_u64(w.s, 63) >= B) break;
@@ -3060,7 +3080,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     const EvMasks em = event_masks(w, ca * kChunk, (ca + cu) * kChunk);
     uint32_t Lf[U];
     first_lanes<U>(w, em, ca, Lf);
-    uint32_t lr[U], raw[U], qf[U];
+    uint32_t lr[U], raw[U], qf[U], cp[U][3];
     if (cu == (uint32_t)U) {
       uint32_t wd[U][16];
 #pragma unroll
@@ -3070,23 +3090,25 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         row_transpose(wd[k]);
       }
       if (em.ms | em.me) {
-        chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf);
+        chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf, cp);
       } else {  // no buffer starts or ends inside these chunks (most of config 3's units)
-        chains_keep<U>(lds, lb, wd, lane, lr, raw);
+        chains_keep<U>(lds, lb, wd, lane, lr, raw, cp);
 #pragma unroll
         for (int k = 0; k < U; ++k) qf[k] = 0u;
       }
     } else {  // the range's single-chunk units
-      uint32_t wd[1][16], l1[1], r1[1], f1[1] = {Lf[0]}, q1[1];
+      uint32_t wd[1][16], l1[1], r1[1], f1[1] = {Lf[0]}, q1[1], c1[1][3];
 #pragma unroll
       for (int q = 0; q < 16; ++q) wd[0][q] = cur[0].d[q];
       row_transpose(wd[0]);
-      chains_first<1>(lds, lb, wd, lane, f1, l1, r1, q1);
+      chains_first<1>(lds, lb, wd, lane, f1, l1, r1, q1, c1);
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         lr[k] = l1[0];
         raw[k] = r1[0];
         qf[k] = q1[0];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) cp[k][m] = c1[0][m];
       }
     }
     if (lane == 0) {
@@ -3094,7 +3116,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
       for (int k = 0; k < U; ++k)
         if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
     }
-    region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, em, lane);
+    region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, cp, em, lane);
 
     u = un;
     ca = can;
@@ -3122,8 +3144,8 @@ struct RegionFold {
   const uint32_t* init;
   uint32_t init_all, flags;
   const uint32_t* raws;
-  const uint32_t* qs;
-  const uint32_t* qe;
+  const uint2* qs;
+  const uint2* qe;
   const uint32_t* tables;
   uint32_t* out;
   uint32_t* ctr;
@@ -3155,25 +3177,21 @@ __device__ uint32_t serial_raw(const uint32_t* t, uint32_t crc, const uint8_t* p
   return crc;
 }
 
-// R = raw(0, the first o bytes of a 64-byte piece) from its 16 words, with
-// a fixed trip count (no divergence, every load issued up front).
-__device__ __forceinline__ uint32_t piece_prefix(const uint32_t* t, const u32x4 (&v)[4], uint32_t o) {
-  const uint32_t q = o >> 2, r = o & 3u;
-  uint32_t crc = 0, x = 0;
+// R = raw(0, the first o bytes of a 64-byte piece), o = 16c + 4m + r, from
+// the chunk kernel's checkpoint x (x_4c = S_4c ^ w[4c]; c = 0: S_0 = 0) and
+// the piece's 16-byte quad c: at most 3 words and 3 bytes, fixed trip count.
+__device__ __forceinline__ uint32_t quad_prefix(const uint32_t* t, uint32_t x, const u32x4& v, uint32_t o) {
+  const uint32_t c = o >> 4, m = (o >> 2) & 3u, r = o & 3u;
+  uint32_t crc = c ? x ^ v[0] : 0u, cur = v[0];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const uint32_t k = 4u * (uint32_t)j + (uint32_t)m;
-      const uint32_t w = v[j][m];
-      const uint32_t nx = fold_slice4(t, crc ^ w);
-      x = k == q ? w : x;
-      crc = k < q ? nx : crc;
-    }
+  for (uint32_t j = 0; j < 3u; ++j) {
+    const uint32_t nx = fold_slice4(t, crc ^ v[j]);
+    crc = j < m ? nx : crc;
+    cur = j + 1u == m ? v[j + 1u] : cur;
   }
 #pragma unroll
   for (uint32_t b = 0; b < 3u; ++b) {
-    const uint32_t nx = fold_step1(t, crc, (x >> (8u * b)) & 255u);
+    const uint32_t nx = fold_step1(t, crc, (cur >> (8u * b)) & 255u);
     crc = b < r ? nx : crc;
   }
   return crc;
@@ -3204,20 +3222,16 @@ __global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
       const uint64_t e = s + L;
       const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
       const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
-      // every load first: the two pieces (the end's clamped into the grid
-      // when it is a chunk end), the events' Qe, the end chunks' raws, the powers
-      const uintptr_t gs = (uintptr_t)a.grid + (s & ~(uint64_t)63);
-      const uintptr_t ge = (uintptr_t)a.grid + (oe == kChunk ? e - 64u : (e & ~(uint64_t)63));
-      u32x4 vs[4], ve[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        vs[j] = ld16c(gs + 16u * (uint32_t)j);
-        ve[j] = ld16c(ge + 16u * (uint32_t)j);
-      }
-      const uint32_t q_s = a.qs[i], q_e = a.qe[i], r0 = a.raws[c0], r1 = a.raws[c1];
+      // every load first: the two events' quads (the end's clamped into the
+      // grid when it is a chunk end) and records, the end chunks' raws, the powers
+      const uintptr_t gs = (uintptr_t)a.grid + (s & ~(uint64_t)15);
+      const uintptr_t ge = (uintptr_t)a.grid + (oe == kChunk ? e - 16u : (e & ~(uint64_t)15));
+      const u32x4 vs = ld16c(gs), ve = ld16c(ge);
+      const uint2 q_s = a.qs[i], q_e = a.qe[i];
+      const uint32_t r0 = a.raws[c0], r1 = a.raws[c1];
       const uint32_t xs = a.tables[kTabXp8 + kChunk - os], xe = a.tables[kTabXm8 + (kChunk - oe)];
       // Ze'(s) = Qe(s) ^ (R(s) ^ ~init) x^(8(4096 - os)): bytes [cs0, s) and ~init at s, at the chunk end
-      const uint32_t zs = (os ? q_s : 0u) ^ gf_mul(xs, piece_prefix(sl, vs, s & 63u) ^ ninit);
+      const uint32_t zs = (os ? q_s.x : 0u) ^ gf_mul(xs, (os ? quad_prefix(sl, q_s.y, vs, s & 63u) : 0u) ^ ninit);
       uint32_t acc = zs;
       if (c0 != c1) {
         acc ^= r0;
@@ -3232,8 +3246,8 @@ __global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
         acc = fold_sh4096(sh, acc);
       }
       // a chunk-end e: the whole chunk, no unshift (xe = x^0)
-      const uint32_t ze = oe == kChunk ? r1 : q_e;
-      const uint32_t re = oe == kChunk ? 0u : piece_prefix(sl, ve, e & 63u);
+      const uint32_t ze = oe == kChunk ? r1 : q_e.x;
+      const uint32_t re = oe == kChunk ? 0u : quad_prefix(sl, q_e.y, ve, e & 63u);
       v = gf_mul(xe, acc ^ ze) ^ re;
     }
     a.out[i] = finish(~v, a.flags);
@@ -3511,11 +3525,11 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
   return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, lc.stream);
 }
 
-// Region workspace: [raws: chunks u32][qs: n u32][qe: n u32] (chunks bounded
+// Region workspace: [raws: chunks u32][qs: n x 8 B][qe: n x 8 B] (chunks bounded
 // by region_len / 4096 + 2 whatever the region's alignment).
 static inline size_t align256(size_t v) { return (v + 255u) / 256u * 256u; }
 size_t region_ws_bytes(uint64_t region_len, uint64_t n) {
-  return align256((region_len / dev::kChunk + 2u) * 4u) + 2u * align256(n * 4u);
+  return align256((region_len / dev::kChunk + 2u) * 4u) + 2u * align256(n * 8u);
 }
 
 hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
@@ -3528,8 +3542,8 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
   const uint64_t nc = (rel0 + region_len + dev::kChunk - 1u) / dev::kChunk;
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* raws = reinterpret_cast<uint32_t*>(w);
-  uint32_t* qs = reinterpret_cast<uint32_t*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
-  uint32_t* qe = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 4u));
+  uint2* qs = reinterpret_cast<uint2*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
+  uint2* qe = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 8u));
   dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, raws, qs, qe,
                     lc.counter};
   dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, nullptr};

@@ -498,3 +498,24 @@ def region_batch(mem: bytes, bufs, inits):
         for kind, c, o in region_events(s, s + L, L):
             qe[(kind, c, o)] = masked_fold(lanes[c], o >> 6)
     return [region_fold(mem, raws, qe, s, L, i) for (s, L), i in zip(bufs, inits)]
+
+
+def chain_checkpoints(piece: bytes):
+    """The chunk kernel's per-lane checkpoints: x_4c = S_4c ^ w[4c] (c = 1..3),
+    S_k = raw(0, piece[0:4k)) -- the chain register before word 4c."""
+    w = [int.from_bytes(piece[4 * k:4 * k + 4], "little") for k in range(16)]
+    return [raw_bytes(0, piece[:16 * c]) ^ w[4 * c] for c in (1, 2, 3)]
+
+
+def quad_prefix(x: int, quad: bytes, o: int) -> int:
+    """crc32c_region_fold_kernel's quad_prefix: raw(0, piece[0:o)) from the
+    checkpoint x (of word 4c, c = o >> 4) and the piece's 16-byte quad c."""
+    c, m, r = o >> 4, (o >> 2) & 3, o & 3
+    v = [int.from_bytes(quad[4 * j:4 * j + 4], "little") for j in range(4)]
+    crc = (x ^ v[0]) if c else 0
+    for j in range(m):
+        crc = slice4(crc ^ v[j])
+    cur = v[m]
+    for b in range(r):
+        crc = T[0][(crc ^ (cur >> (8 * b))) & 0xFF] ^ (crc >> 8)
+    return crc

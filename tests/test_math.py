@@ -205,3 +205,16 @@ def test_region_path_model(port, seed):
     got = km.region_batch(mem, bufs, inits)
     want = [port.extend(i, mem[s:s + L]) for (s, L), i in zip(bufs, inits)]
     assert got == want
+
+
+def test_region_quad_prefix_from_checkpoints(port):
+    """The fold kernel's R(p) from the chunk kernel's chain checkpoint and one
+    16-byte quad equals the piece prefix's raw at every offset 0..63."""
+    rng = random.Random(12)
+    for _ in range(20):
+        piece = bytes(rng.getrandbits(8) for _ in range(64))
+        cps = km.chain_checkpoints(piece)
+        for o in range(64):
+            c = o >> 4
+            x = cps[c - 1] if c else 0
+            assert km.quad_prefix(x, piece[16 * c:16 * c + 16], o) == km.raw_bytes(0, piece[:o]), o

@@ -96,7 +96,8 @@ size_t region_ws_bytes(uint64_t region_len, uint64_t n);
 hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* ws);
-constexpr uint32_t kRegionFlag = 16, kRegionDone = 17;  // counter-block words (the fused kernel uses word 0)
+constexpr uint32_t kRegionFlag = 16;  // counter-block word (the fused kernel uses word 0): the generation of
+                                      // the last region call whose batch was not region-shaped
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

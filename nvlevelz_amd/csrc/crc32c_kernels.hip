@@ -32,6 +32,7 @@
 // table t, byte b, lane l:  (t>>1)<<16 | b<<8 | (t&1)<<7 | (l&31)<<2, formed
 // with ONE v_perm_b32 per lookup from the data word and a per-lane base.
 #include <hip/hip_ext.h>
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -2743,6 +2744,7 @@ struct RegionGeom {
   uint2* qs;       // [n] buffer i's start event: {Qe, lane L's chain checkpoint x_4c}
   uint2* qe;       // [n] its end event
   uint32_t* ctr;   // the stream's counter block
+  uint32_t gen;    // this call's generation: ctr[kRegionFlag] = gen marks the batch as not region-shaped
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* g64_ptr;
@@ -2897,17 +2899,6 @@ __device__ __forceinline__ void chains_first(const uint8_t* lds, const LaneBase&
   }
 }
 
-// Event masks of a window over the unit's byte range [A, B): starts and
-// ends of big buffers strictly inside a chunk.
-struct EvMasks {
-  uint64_t ms, me;
-};
-__device__ __forceinline__ EvMasks event_masks(const Win& w, uint64_t A, uint64_t B) {
-  const bool sv = w.big && (w.s & (kChunk - 1u)) != 0u && w.s >= A && w.s < B;
-  const bool ev = w.big && (w.e & (kChunk - 1u)) != 0u && w.e > A && w.e < B;
-  return EvMasks{__ballot(sv), __ballot(ev)};
-}
-
 // Qe(L): the butterfly over the lanes below L, the others zeroed.
 __device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr, uint32_t L, int lane) {
   uint32_t g = (uint32_t)lane < L ? lr : 0u;
@@ -2920,82 +2911,101 @@ __device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr,
   return uniform_u32(g);
 }
 
-// The events of chunks [ca, ca + cu) (lr[k]: chunk ca + k's lane raws): Qe
-// for every start and end of a big buffer strictly inside a chunk, in
-// position order (consecutive events on one lane of one chunk share Qe).
-// `w` is the window at `cur`; further windows are loaded while the last
-// buffer of the current one still starts before the unit's end.
+// This lane's events in the unit [A, B) (its window buffer): in-unit
+// positions of its start / end when they are events.
+struct LaneEv {
+  uint32_t ps, pe;
+  bool sv, ev;
+};
+__device__ __forceinline__ LaneEv lane_events(const Win& w, uint64_t A, uint64_t B) {
+  LaneEv le;
+  le.sv = w.big && (w.s & (kChunk - 1u)) != 0u && w.s >= A && w.s < B;
+  le.ev = w.big && (w.e & (kChunk - 1u)) != 0u && w.e > A && w.e < B;
+  le.ps = (uint32_t)(w.s - A);
+  le.pe = (uint32_t)(w.e - A);
+  return le;
+}
+
+// The first event lane of each chunk of the unit (0 when none): its masked
+// butterfly runs fused with the full ones (chains_first).  Events are in
+// lane order by position (a lane's start before its end).
+template <int U>
+__device__ __forceinline__ void first_lanes(const LaneEv& le, uint32_t (&Lf)[U]) {
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const bool sk = le.sv && (le.ps >> 12) == (uint32_t)k, ek = le.ev && (le.pe >> 12) == (uint32_t)k;
+    const uint64_t m = __ballot(sk || ek);
+    Lf[k] = 0u;
+    if (m) Lf[k] = (lane_u32(sk ? le.ps : le.pe, (uint32_t)__builtin_ctzll(m)) & (kChunk - 1u)) >> 6;
+  }
+}
+
+// The events of chunks [ca, ca + cu) (lr[k], cp[k]: chunk ca + k's lane raws
+// and chain checkpoints): every window lane records its own start and end
+// ({Qe, its piece lane's checkpoint x_4c}, one coalesced store) when the
+// event sits on its chunk's first event lane -- Qe = qf[k] from the fused
+// butterflies, the checkpoint read once per chunk; the other events (a second
+// boundary lane in one chunk) go one by one through masked_fold.  `w` is the
+// window at `cur`; further windows are loaded while the last buffer of the
+// current one still starts before the unit's end.
 template <int U>
 __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t* lds, Win w, uint64_t cur,
                                               uint64_t ca, uint32_t cu, const uint32_t (&lr)[U],
                                               const uint32_t (&Lf)[U], const uint32_t (&qf)[U],
-                                              const uint32_t (&cp)[U][3], EvMasks em, int lane) {
+                                              const uint32_t (&cp)[U][3], LaneEv le, int lane) {
   const uint64_t A = ca * kChunk, B = (ca + cu) * kChunk;
-  uint32_t pk = ~0u, pL = ~0u, pq = 0;
+  uint32_t cpf[U][3];
+#pragma unroll
+  for (int k = 0; k < U; ++k)
+#pragma unroll
+    for (int m = 0; m < 3; ++m) cpf[k][m] = lane_u32(cp[k][m], Lf[k]);
+  // fast record of the event at in-unit position pos (uniform-indexed selects)
+  auto rec = [&](uint32_t pos, uint2& r) -> bool {
+    const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6, c = (pos >> 4) & 3u;
+    uint32_t lf = Lf[0], q = qf[0], x = 0u;
+#pragma unroll
+    for (int kk = 0; kk < U; ++kk) {
+      if (kk) {
+        lf = k == (uint32_t)kk ? Lf[kk] : lf;
+        q = k == (uint32_t)kk ? qf[kk] : q;
+      }
+#pragma unroll
+      for (int m = 0; m < 3; ++m) x = (k == (uint32_t)kk && c == (uint32_t)m + 1u) ? cpf[kk][m] : x;
+    }
+    r = make_uint2(q, x);
+    return L == lf;
+  };
   for (;;) {
-    const uint64_t ms = em.ms, me = em.me;
+    uint2 rs, re;
+    const bool fs = le.sv && rec(le.ps, rs), fe = le.ev && rec(le.pe, re);
+    if (fs) g.qs[cur + (uint64_t)lane] = rs;
+    if (fe) g.qe[cur + (uint64_t)lane] = re;
+    const uint64_t ms = __ballot(le.sv && !fs), me = __ballot(le.ev && !fe);
     uint64_t all = ms | me;
-    while (all) {
+    while (all) {  // events on another lane than their chunk's first
       const uint32_t j = (uint32_t)__builtin_ctzll(all);
       all &= all - 1u;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {  // start, then end
         if (!(((t ? me : ms) >> j) & 1u)) continue;
-        const uint32_t pos = (uint32_t)(lane_u64(t ? w.e : w.s, j) - A);
-        const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6;
-        if (k != pk || L != pL) {
-          uint32_t v = lr[0], lf = Lf[0], q0 = qf[0];
+        const uint32_t pos = lane_u32(t ? le.pe : le.ps, j);
+        const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6, c = (pos >> 4) & 3u;
+        uint32_t v = lr[0], x = 0u;
 #pragma unroll
-          for (int q = 1; q < U; ++q) {
-            v = k == (uint32_t)q ? lr[q] : v;
-            lf = k == (uint32_t)q ? Lf[q] : lf;
-            q0 = k == (uint32_t)q ? qf[q] : q0;
-          }
-          pq = L == lf ? q0 : masked_fold(lds, v, L, lane);  // the first event lane came with the butterflies
-          pk = k;
-          pL = L;
-        }
-        // lane L's checkpoint before word 4c of its piece (c = 0: the zero state)
-        const uint32_t c = (pos >> 4) & 3u;
-        uint32_t x = 0u;
-#pragma unroll
-        for (int q = 0; q < U; ++q)
+        for (int q = 0; q < U; ++q) {
+          if (q) v = k == (uint32_t)q ? lr[q] : v;
 #pragma unroll
           for (int m = 0; m < 3; ++m) x = (k == (uint32_t)q && c == (uint32_t)m + 1u) ? cp[q][m] : x;
+        }
+        const uint32_t qe = masked_fold(lds, v, L, lane);
         const uint32_t xl = lane_u32(x, L);
-        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = make_uint2(pq, c ? xl : 0u);
+        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = make_uint2(qe, xl);
       }
     }
     if (cur + 64u >= g.n || lane_u64(w.s, 63) >= B) break;
     cur += 64u;  // the unit's buffers run past the window (short buffers): the next one
     w = make_win(g, load_win(g, cur, lane), cur, lane);
-    em = event_masks(w, A, B);
-  }
-}
-
-// First event lane per chunk of the unit (64: none) from the window's masks.
-template <int U>
-__device__ __forceinline__ void first_lanes(const Win& w, const EvMasks& em, uint64_t ca, uint32_t (&Lf)[U]) {
-  const uint64_t A = ca * kChunk;
-#pragma unroll
-  for (int k = 0; k < U; ++k) Lf[k] = 0u;
-  uint64_t all = em.ms | em.me;
-  uint32_t need = (1u << U) - 1u;
-  while (all && need) {
-    const uint32_t j = (uint32_t)__builtin_ctzll(all);
-    all &= all - 1u;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (!(((t ? em.me : em.ms) >> j) & 1u)) continue;
-      const uint32_t pos = (uint32_t)(lane_u64(t ? w.e : w.s, j) - A);
-      const uint32_t k = pos >> 12;
-      if ((need >> k) & 1u) {
-#pragma unroll
-        for (int q = 0; q < U; ++q)
-          if ((uint32_t)q == k) Lf[q] = (pos & (kChunk - 1u)) >> 6;
-        need &= ~(1u << k);
-      }
-    }
+    le = lane_events(w, A, B);
   }
 }
 
@@ -3059,7 +3069,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
       bad |= o > g.region_len || L > g.region_len - o;
       bad |= o < ldg64(g.offsets, i - 1) + ldg64(g.lengths, i - 1);
     }
-    if (__ballot(bad) && lane == 0) g.ctr[kRegionFlag] = 1u;
+    if (__ballot(bad) && lane == 0) g.ctr[kRegionFlag] = g.gen;
   }
   const LaneBase lb = make_lane_base(lane);
 
@@ -3077,9 +3087,10 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     Chunk nxt[U];
     load_unit(can, cun, nxt);
 
-    const EvMasks em = event_masks(w, ca * kChunk, (ca + cu) * kChunk);
+    const LaneEv le = lane_events(w, ca * kChunk, (ca + cu) * kChunk);
     uint32_t Lf[U];
-    first_lanes<U>(w, em, ca, Lf);
+    first_lanes<U>(le, Lf);
+    const bool any_ev = __ballot(le.sv || le.ev) != 0u;
     uint32_t lr[U], raw[U], qf[U], cp[U][3];
     if (cu == (uint32_t)U) {
       uint32_t wd[U][16];
@@ -3089,7 +3100,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
         row_transpose(wd[k]);
       }
-      if (em.ms | em.me) {
+      if (any_ev) {
         chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf, cp);
       } else {  // no buffer starts or ends inside these chunks (most of config 3's units)
         chains_keep<U>(lds, lb, wd, lane, lr, raw, cp);
@@ -3116,7 +3127,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
       for (int k = 0; k < U; ++k)
         if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
     }
-    region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, cp, em, lane);
+    region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, cp, le, lane);
 
     u = un;
     ca = can;
@@ -3148,7 +3159,8 @@ struct RegionFold {
   const uint2* qe;
   const uint32_t* tables;
   uint32_t* out;
-  uint32_t* ctr;
+  const uint32_t* ctr;
+  uint32_t gen;
 };
 
 __device__ __forceinline__ uint32_t fold_slice4(const uint32_t* t, uint32_t x) {
@@ -3208,7 +3220,9 @@ __global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
     sl[t] = a.tables[kGSlice + t];
     sh[t] = a.tables[kGComb + 6u * 1024u + t];
   }
-  const bool bad = ldc(a.ctr, kRegionFlag) != 0u;
+  // the chunk kernel of THIS call found the batch out of order (a flag left
+  // by an earlier call carries another generation: nothing is ever reset)
+  const bool bad = ldc(a.ctr, kRegionFlag) == a.gen;
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.n) {
@@ -3251,16 +3265,6 @@ __global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
       v = gf_mul(xe, acc ^ ze) ^ re;
     }
     a.out[i] = finish(~v, a.flags);
-  }
-  // The last workgroup re-zeroes the flag and the done count (every
-  // workgroup read the flag before its add).
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t d = __hip_atomic_fetch_add(a.ctr + kRegionDone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == gridDim.x - 1u) {
-      a.ctr[kRegionFlag] = 0u;
-      a.ctr[kRegionDone] = 0u;
-    }
   }
 }
 
@@ -3544,8 +3548,13 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
   uint32_t* raws = reinterpret_cast<uint32_t*>(w);
   uint2* qs = reinterpret_cast<uint2*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
   uint2* qe = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 8u));
+  // A process-wide call generation (never 0, the zeroed block's value): the
+  // fold kernel trusts the flag word only when it carries this call's.
+  static std::atomic<uint32_t> s_gen{0};
+  uint32_t gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
+  if (gen == 0u) gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
   dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, raws, qs, qe,
-                    lc.counter};
+                    lc.counter, gen};
   dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, nullptr};
   const uint32_t grid = grid_for(lc.num_cu, nc);  // >= 1: the waves also check the batch
   if (lc.ev_start)
@@ -3556,7 +3565,7 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   dev::RegionFold f{reinterpret_cast<const uint8_t*>(O), rel0, offsets, lengths, n, init, init_all, flags, raws, qs,
-                    qe, lc.tables, out, lc.counter};
+                    qe, lc.tables, out, lc.counter, gen};
   const dim3 fg((uint32_t)((n + 255u) / 256u));
   if (lc.ev_stop)
     hipExtLaunchKernelGGL(dev::crc32c_region_fold_kernel, fg, dim3(256), 0, lc.stream, nullptr, lc.ev_stop, 0u, f);

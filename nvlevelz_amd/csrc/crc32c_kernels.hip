@@ -3088,9 +3088,11 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     load_unit(can, cun, nxt);
 
     const LaneEv le = lane_events(w, ca * kChunk, (ca + cu) * kChunk);
-    uint32_t Lf[U];
-    first_lanes<U>(le, Lf);
     const bool any_ev = __ballot(le.sv || le.ev) != 0u;
+    uint32_t Lf[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) Lf[k] = 0u;
+    if (any_ev) first_lanes<U>(le, Lf);
     uint32_t lr[U], raw[U], qf[U], cp[U][3];
     if (cu == (uint32_t)U) {
       uint32_t wd[U][16];
@@ -3127,7 +3129,10 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
       for (int k = 0; k < U; ++k)
         if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
     }
-    region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, cp, le, lane);
+    // (a unit with no event and no buffer running past its window -- most of
+    // config 3's -- has nothing to record)
+    if (any_ev || (cursor + 64u < g.n && lane_u64(w.s, 63) < (ca + cu) * kChunk))
+      region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, cp, le, lane);
 
     u = un;
     ca = can;

@@ -1,0 +1,68 @@
+"""Interleaved timing of library variants on the region path (one process):
+    python tools/diag/ab_region.py CONFIG lib_A.so lib_B.so ...   (CONFIG: vR, rR, 3R)
+M rounds x R back-to-back calls per variant, HIP events around each round
+(mean per call = the sustained period) and around single calls (median)."""
+import ctypes, json, os, sys
+import numpy as np, torch
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.getcwd()))
+from nvlevelz_amd import _lib
+
+
+def load(path):
+    lib = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        if hasattr(lib, name):
+            f = getattr(lib, name); f.restype = res; f.argtypes = args
+    return lib
+
+
+cfg, paths = sys.argv[1], sys.argv[2:]
+dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
+libs = [load(p) for p in paths]
+for lib in libs:
+    assert lib.nvl_crc32c_init(0) == 0
+import oracle
+if cfg == "3R":
+    lens = oracle.port().cfg3_lengths(0x5EED0003, 1 << 30).astype(np.int64); gap = 0; total = 1 << 30
+    alg = total + 12 * lens.size
+else:
+    lens = (np.full(100_000, 4097) if cfg == "vR" else np.random.default_rng(7).integers(3364, 4110, 100_000)
+            ).astype(np.int64); gap = 4
+    total = int((lens + gap).sum()); alg = int(lens.sum()) + 20 * lens.size
+offs = np.concatenate([[0], np.cumsum(lens + gap)[:-1]]).astype(np.int64)
+n = lens.size
+buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+libs[0].nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, 0x5EED00B1, None)
+o = torch.from_numpy(offs).to(dev); m = torch.from_numpy(lens).to(dev)
+outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
+wsb = libs[0].nvl_crc32c_region_workspace_bytes(total, n)
+ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+st = torch.cuda.current_stream().cuda_stream
+run = lambda k: libs[k].nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.data_ptr(), None, 0,
+                                              outs[k].data_ptr(), n, 0, ws.data_ptr(), wsb, st)
+rounds, reps = int(os.environ.get("AB_ROUNDS", "6")), int(os.environ.get("AB_REPS", "30"))
+per = [[] for _ in libs]
+single = [[] for _ in libs]
+for k in range(len(libs)):
+    for _ in range(5): run(k)
+torch.cuda.synchronize()
+for r in range(rounds):
+    for k in range(len(libs)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps): run(k)
+        e1.record()
+        torch.cuda.synchronize()
+        per[k].append(e0.elapsed_time(e1) * 1e3 / reps)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
+        for j in range(5):
+            ev[2 * j].record(); run(k); ev[2 * j + 1].record()
+        torch.cuda.synchronize()
+        single[k] += [ev[2 * j].elapsed_time(ev[2 * j + 1]) * 1e3 for j in range(5)]
+ref = outs[0].cpu()
+for k, p in enumerate(paths):
+    t = float(np.median(per[k]))
+    print(json.dumps({"config": cfg, "variant": os.path.basename(p), "period_us": round(t, 2),
+                      "period_rounds": [round(x, 1) for x in per[k]], "single_median_us": round(float(np.median(single[k])), 2),
+                      "frac": round(alg / (t * 1e-6) / 8e12, 4), "same_as_first": bool(torch.equal(outs[k].cpu(), ref))}),
+          flush=True)

@@ -18,7 +18,13 @@ sed -e 's|^    const WinRaw nwr = load_win(g, ncur, lane);|    const WinRaw nwr 
 [ $(grep -c 'WinRaw nwr = WinRaw{0u, 0u};\|uint64_t cursor = 0u;' $R/build/abl_rnowin.hip) -eq 2 ] || { echo "rnowin: anchors" >&2; exit 1; }
 sed -e 's|^  dev::RegionFold f{|  return hipGetLastError();\n  dev::RegionFold f{|' $SRC > $R/build/abl_rnofold.hip
 [ $(grep -c '^  return hipGetLastError();$' $R/build/abl_rnofold.hip) -ge 1 ] || { echo "rnofold: anchors" >&2; exit 1; }
-for v in rnoev rnowin rnofold; do
+#   rbare    rnowin without the batch check (no metadata reads at all): the bare chunk pass
+sed -e 's|^  const uint64_t co = ldg64(g.offsets, ci), cl = ldg64(g.lengths, ci);|  const uint64_t co = 0, cl = 0;|' \
+    -e 's|^  const uint64_t po = ldg64(g.offsets, cp), pl = ldg64(g.lengths, cp);|  const uint64_t po = 0, pl = 0;|' \
+    -e 's|^    for (uint64_t i = i0 + 64u + (uint64_t)lane; i < i1; i += 64u) {  // slices of more than 64 buffers|    for (uint64_t i = i1; i < i1; i += 64u) {|' \
+    $R/build/abl_rnowin.hip > $R/build/abl_rbare.hip
+[ $(grep -c 'const uint64_t co = 0, cl = 0;\|const uint64_t po = 0, pl = 0;\|for (uint64_t i = i1; i < i1;' $R/build/abl_rbare.hip) -eq 3 ] || { echo "rbare: anchors" >&2; exit 1; }
+for v in rnoev rnowin rnofold rbare; do
   make -C $R/nvlevelz_amd/csrc variant NAME=$v VSRC=$R/build/abl_$v.hip VFLAGS="-I$R/nvlevelz_amd/csrc" > /dev/null
 done
-echo built build/libnvl_crc32c_{rnoev,rnowin,rnofold}.so
+echo built build/libnvl_crc32c_{rnoev,rnowin,rnofold,rbare}.so

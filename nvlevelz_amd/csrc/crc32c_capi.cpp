@@ -47,6 +47,12 @@ void build_device_tables(uint32_t* w) {
       q = (q & kOne) ? (((q ^ kPolyReflected) << 1) | 1u) : (q << 1);
     }
   }
+  // the region kernel's per-lane shifts to the chunk end: T[n][v][j] = shift(v << 4n, 64(63 - j))
+  for (uint32_t j = 0; j < 64; ++j) {
+    const uint32_t m = w[kTabXp8 + 64u * (63u - j)];
+    for (uint32_t n = 0; n < 8; ++n)
+      for (uint32_t v = 0; v < 16; ++v) w[kTabNib + (n * 16u + v) * 64u + j] = gf_mul(m, v << (4u * n));
+  }
 }
 
 namespace {

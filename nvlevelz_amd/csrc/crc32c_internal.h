@@ -19,8 +19,12 @@ namespace nvl {
 //   [8192,  8256)  x2n[64]            x^(2^k) mod P
 //   [8256, 12353)  xp8[4097]          x^(8d) mod P, d = 0..4096        (region fold)
 //   [12353,16449)  xm8[4096]          x^(-8d) mod P, d = 0..4095       (region fold)
+//   [16452,24644)  nib[8][16][64]     T[n][v][j] = shift(v << 4n, 64(63 - j))  (region kernel:
+//                                     lane j's piece raw to the chunk end; 16-byte aligned, copied
+//                                     verbatim into LDS)
 constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + 4097;
-constexpr uint32_t kTableWords = kTabXm8 + 4096;
+constexpr uint32_t kTabNib = (kTabXm8 + 4096u + 3u) & ~3u;
+constexpr uint32_t kTableWords = kTabNib + 8u * 16u * 64u;
 
 // A portion of one buffer processed inside one work unit (fix-up input).
 struct Rec {

@@ -872,10 +872,10 @@ __device__ __forceinline__ uint32_t normalize(const uint8_t* lds, const uint32_t
   return nvl::shift_bytes(tables + kGX2n, acc, (uint64_t)after * kChunk);
 }
 
-__device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane) {
+__device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane, uint32_t ctr = kCtrOff) {
   uint32_t v = 0;
   if (lane == 0)
-    v = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + kCtrOff), 1u, __ATOMIC_RELAXED,
+    v = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + ctr), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
   return uniform_u32(v);
 }
@@ -2816,99 +2816,112 @@ __device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane) {
   return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
-// Chains and butterflies of U chunks, keeping each lane's piece raw (the
-// input of the events' masked butterflies).
+// The region kernel's LDS image: no butterfly tables.  Each lane moves its
+// piece raw to the chunk end by its OWN constant, x^(8*64*(63 - lane)), from
+// nibble tables T[n][v][lane] = shift(v << 4n, 64(63 - lane)) (8 x 16 rows of
+// 64 lanes: a lane reads only its own column, conflict-free); the chunk raw
+// and every lane prefix are then plain XORs over lanes (xor_scan, DPP).
+// Lane 63 (identity) never reads its column, whose first slot holds the
+// workgroup's unit counter.  The slice replicas follow at 32 KiB.
+constexpr uint32_t kRNibOff = 0;
+constexpr uint32_t kRCtrOff = 252;  // T[0][0][63]
+constexpr uint32_t kRSliceOff = 32768;
+constexpr uint32_t kRLdsBytes = kRSliceOff + kRepBytes;  // 163840 B
+static_assert(kRLdsBytes <= 160u * 1024u, "region LDS image exceeds 160 KiB");
+constexpr uint32_t kGNib = kTabNib;  // the blob's nibble tables (crc32c_internal.h)
+
+// The region image: slice replicas at kRSliceOff, nibble tables verbatim,
+// the unit counter patched into its slot by the thread that copies it.
+template <int NW>
+__device__ __forceinline__ void fill_lds_region(uint8_t* lds, const uint32_t* __restrict__ g, uint32_t ctr0) {
+  constexpr int kT = kWave * NW;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < (8192 + kT - 1) / kT; ++q) {
+    const uint32_t s = (uint32_t)(t + q * kT);
+    if ((8192 % kT) != 0 && s >= 8192u) break;
+    const uint32_t off = s << 4;
+    const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
+    const uint32_t b = (off >> 8) & 0xFFu;
+    const uint32_t v = g[kGSlice + tab * 256u + b];
+    *reinterpret_cast<uint4*>(lds + kRSliceOff + off) = make_uint4(v, v, v, v);
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(g + kGNib);
+  uint4* dst = reinterpret_cast<uint4*>(lds + kRNibOff);
+  for (int q = t; q < 2048; q += kT) {
+    uint4 v = src[q];
+    if (q == (int)(kRCtrOff >> 4)) v.w = ctr0;  // units 0..ctr0-1 are pre-assigned
+    dst[q] = v;
+  }
+}
+
+// shift(lr, 64(63 - lane)): this lane's piece raw moved to the chunk end.
+// Address of row (n, v): v << 8 | lane << 2 -- v_perm puts the nibble byte
+// over the lane byte; n is the ds_read immediate.
+__device__ __forceinline__ uint32_t to_chunk_end(const uint8_t* lds, uint32_t lr, uint32_t jb, int lane) {
+  const uint32_t lo = lr & 0x0F0F0F0Fu, hi = (lr >> 4) & 0x0F0F0F0Fu;
+  const uint8_t* nb = lds + kRNibOff;
+  const uint32_t r0 = lds_u32(nb + 0u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0400u));
+  const uint32_t r1 = lds_u32(nb + 1u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0400u));
+  const uint32_t r2 = lds_u32(nb + 2u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0500u));
+  const uint32_t r3 = lds_u32(nb + 3u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0500u));
+  const uint32_t r4 = lds_u32(nb + 4u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0600u));
+  const uint32_t r5 = lds_u32(nb + 5u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0600u));
+  const uint32_t r6 = lds_u32(nb + 6u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0700u));
+  const uint32_t r7 = lds_u32(nb + 7u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0700u));
+  const uint32_t t = xor3(xor3(r0, r1, r2), xor3(r3, r4, r5), r6) ^ r7;
+  return lane == 63 ? lr : t;
+}
+
+// Inclusive XOR scan over the wave's 64 lanes (rows of 16 by row_shr, then
+// row_bcast:15 / :31 across rows).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_or0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t xor_scan(uint32_t x) {
+  x ^= dpp_or0<0x111, 0xF>(x);  // row_shr:1
+  x ^= dpp_or0<0x112, 0xF>(x);  // row_shr:2
+  x ^= dpp_or0<0x114, 0xF>(x);  // row_shr:4
+  x ^= dpp_or0<0x118, 0xF>(x);  // row_shr:8
+  x ^= dpp_or0<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3
+  x ^= dpp_or0<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+
+// Chains of U chunks, then per chunk: raw[u] = raw(0, chunk) (wave-uniform)
+// and pre[u] = this lane's exclusive prefix, the chunk bytes [0, 64 lane) at
+// the chunk end -- Qe(L) of an event on lane L is pre at lane L.
 // cp[u][c - 1] = the chain register before word 4c (c = 1, 2, 3): the state
 // after 4c words with word 4c XORed in (x_4c = S_4c ^ w[4c]); an event's
 // record carries its lane's checkpoint, so the fold kernel re-runs at most 3
-// words of the piece instead of 15.
+// words of the piece instead of 15.  `lsl` = the LDS image shifted so that
+// the chain's kSliceOff lands on kRSliceOff.
 template <int U>
-__device__ __forceinline__ void chains_keep(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
-                                            int lane, uint32_t (&lr)[U], uint32_t (&raw)[U], uint32_t (&cp)[U][3]) {
+__device__ __forceinline__ void chains_scan(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
+                                            int lane, uint32_t (&raw)[U], uint32_t (&pre)[U],
+                                            uint32_t (&cp)[U][3]) {
+  const uint8_t* lsl = lds + (kRSliceOff - kSliceOff);
   uint32_t crc[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) crc[u] = w[u][0];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lsl, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
     if (k == 3 || k == 7 || k == 11) {
 #pragma unroll
       for (int u = 0; u < U; ++u) cp[u][k >> 2] = crc[u];
     }
   }
-#pragma unroll
-  for (int u = 0; u < U; ++u) lr[u] = crc[u];
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<0, 0, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<1, 1, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<2, 2, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<3, 3, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<4, 4, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = fold_level<5, 5, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) raw[u] = crc[u];
-}
-
-// The same with each chunk's first event fused in: besides raw[u], the
-// butterfly over the lanes below Lf[u] (the others zeroed) = Qe at the
-// chunk's first event lane, interleaved with the full butterflies (Lf = 0
-// when the chunk has no event: Qf = 0).
-template <int U>
-__device__ __forceinline__ void chains_first(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16],
-                                             int lane, const uint32_t (&Lf)[U], uint32_t (&lr)[U],
-                                             uint32_t (&raw)[U], uint32_t (&qf)[U], uint32_t (&cp)[U][3]) {
-  uint32_t crc[2 * U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) crc[u] = w[u][0];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
-    if (k == 3 || k == 7 || k == 11) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) cp[u][k >> 2] = crc[u];
-    }
-  }
+  const uint32_t jb = (uint32_t)lane << 2;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    lr[u] = crc[u];
-    crc[U + u] = (uint32_t)lane < Lf[u] ? crc[u] : 0u;
+    const uint32_t t = to_chunk_end(lds, crc[u], jb, lane);
+    const uint32_t inc = xor_scan(t);
+    raw[u] = lane_u32(inc, 63u);
+    pre[u] = inc ^ t;
   }
-#pragma unroll
-  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<0, 0, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<1, 1, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<2, 2, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<3, 3, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<4, 4, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < 2 * U; ++u) crc[u] = fold_level<5, 5, false>(lds, crc[u], lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    raw[u] = crc[u];
-    qf[u] = uniform_u32(crc[U + u]);
-  }
-}
-
-// Qe(L): the butterfly over the lanes below L, the others zeroed.
-__device__ __forceinline__ uint32_t masked_fold(const uint8_t* lds, uint32_t lr, uint32_t L, int lane) {
-  uint32_t g = (uint32_t)lane < L ? lr : 0u;
-  g = fold_level<0, 0, false>(lds, g, lane);
-  g = fold_level<1, 1, false>(lds, g, lane);
-  g = fold_level<2, 2, false>(lds, g, lane);
-  g = fold_level<3, 3, false>(lds, g, lane);
-  g = fold_level<4, 4, false>(lds, g, lane);
-  g = fold_level<5, 5, false>(lds, g, lane);
-  return uniform_u32(g);
 }
 
 // This lane's events in the unit [A, B) (its window buffer): in-unit
@@ -2926,9 +2939,8 @@ __device__ __forceinline__ LaneEv lane_events(const Win& w, uint64_t A, uint64_t
   return le;
 }
 
-// The first event lane of each chunk of the unit (0 when none): its masked
-// butterfly runs fused with the full ones (chains_first).  Events are in
-// lane order by position (a lane's start before its end).
+// The first event lane of each chunk of the unit (0 when none).  Events are
+// in lane order by position (a lane's start before its end).
 template <int U>
 __device__ __forceinline__ void first_lanes(const LaneEv& le, uint32_t (&Lf)[U]) {
 #pragma unroll
@@ -2940,25 +2952,25 @@ __device__ __forceinline__ void first_lanes(const LaneEv& le, uint32_t (&Lf)[U])
   }
 }
 
-// The events of chunks [ca, ca + cu) (lr[k], cp[k]: chunk ca + k's lane raws
-// and chain checkpoints): every window lane records its own start and end
-// ({Qe, its piece lane's checkpoint x_4c}, one coalesced store) when the
-// event sits on its chunk's first event lane -- Qe = qf[k] from the fused
-// butterflies, the checkpoint read once per chunk; the other events (a second
-// boundary lane in one chunk) go one by one through masked_fold.  `w` is the
-// window at `cur`; further windows are loaded while the last buffer of the
-// current one still starts before the unit's end.
+// The events of chunks [ca, ca + cu) (pre[k], cp[k]: chunk ca + k's lane
+// prefixes and chain checkpoints): every window lane records its own start
+// and end ({Qe, its piece lane's checkpoint x_4c}, one coalesced store) when
+// the event sits on its chunk's first event lane -- that lane's values read
+// once per chunk; the other events (a second boundary lane in one chunk) go
+// one by one.  `w` is the window at `cur`; further windows are loaded while
+// the last buffer of the current one still starts before the unit's end.
 template <int U>
-__device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t* lds, Win w, uint64_t cur,
-                                              uint64_t ca, uint32_t cu, const uint32_t (&lr)[U],
-                                              const uint32_t (&Lf)[U], const uint32_t (&qf)[U],
+__device__ __forceinline__ void region_events(const RegionGeom& g, Win w, uint64_t cur, uint64_t ca, uint32_t cu,
+                                              const uint32_t (&pre)[U], const uint32_t (&Lf)[U],
                                               const uint32_t (&cp)[U][3], LaneEv le, int lane) {
   const uint64_t A = ca * kChunk, B = (ca + cu) * kChunk;
-  uint32_t cpf[U][3];
+  uint32_t qf[U], cpf[U][3];
 #pragma unroll
-  for (int k = 0; k < U; ++k)
+  for (int k = 0; k < U; ++k) {
+    qf[k] = lane_u32(pre[k], Lf[k]);
 #pragma unroll
     for (int m = 0; m < 3; ++m) cpf[k][m] = lane_u32(cp[k][m], Lf[k]);
+  }
   // fast record of the event at in-unit position pos (uniform-indexed selects)
   auto rec = [&](uint32_t pos, uint2& r) -> bool {
     const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6, c = (pos >> 4) & 3u;
@@ -2990,16 +3002,15 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, const uint8_t
         if (!(((t ? me : ms) >> j) & 1u)) continue;
         const uint32_t pos = lane_u32(t ? le.pe : le.ps, j);
         const uint32_t k = pos >> 12, L = (pos & (kChunk - 1u)) >> 6, c = (pos >> 4) & 3u;
-        uint32_t v = lr[0], x = 0u;
+        uint32_t v = pre[0], x = 0u;
 #pragma unroll
         for (int q = 0; q < U; ++q) {
-          if (q) v = k == (uint32_t)q ? lr[q] : v;
+          if (q) v = k == (uint32_t)q ? pre[q] : v;
 #pragma unroll
           for (int m = 0; m < 3; ++m) x = (k == (uint32_t)q && c == (uint32_t)m + 1u) ? cp[q][m] : x;
         }
-        const uint32_t qe = masked_fold(lds, v, L, lane);
-        const uint32_t xl = lane_u32(x, L);
-        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = make_uint2(qe, xl);
+        const uint2 r = make_uint2(lane_u32(v, L), lane_u32(x, L));
+        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = r;
       }
     }
     if (cur + 64u >= g.n || lane_u64(w.s, 63) >= B) break;
@@ -3056,7 +3067,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint64_t ci = min(i0 + (uint64_t)lane, g.n - 1u), cp = ci ? ci - 1u : 0u;
   const uint64_t co = ldg64(g.offsets, ci), cl = ldg64(g.lengths, ci);
   const uint64_t po = ldg64(g.offsets, cp), pl = ldg64(g.lengths, cp);
-  fill_lds<kWavesPerWG>(lds, ka.tables);
+  fill_lds_region<kWavesPerWG>(lds, ka.tables, kWavesPerWG);
   __syncthreads();
   {
     bool bad = false;
@@ -3074,7 +3085,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const LaneBase lb = make_lane_base(lane);
 
   while (u < nunits) {
-    const uint32_t un = pull_unit(lds, lane);
+    const uint32_t un = pull_unit(lds, lane, kRCtrOff);
     const Win w = make_win(g, wr, cursor, lane);
     const uint64_t can = first_of(un);
     const uint32_t cun = count_of(un);
@@ -3093,7 +3104,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
 #pragma unroll
     for (int k = 0; k < U; ++k) Lf[k] = 0u;
     if (any_ev) first_lanes<U>(le, Lf);
-    uint32_t lr[U], raw[U], qf[U], cp[U][3];
+    uint32_t raw[U], pre[U], cp[U][3];
     if (cu == (uint32_t)U) {
       uint32_t wd[U][16];
 #pragma unroll
@@ -3102,24 +3113,17 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
         row_transpose(wd[k]);
       }
-      if (any_ev) {
-        chains_first<U>(lds, lb, wd, lane, Lf, lr, raw, qf, cp);
-      } else {  // no buffer starts or ends inside these chunks (most of config 3's units)
-        chains_keep<U>(lds, lb, wd, lane, lr, raw, cp);
-#pragma unroll
-        for (int k = 0; k < U; ++k) qf[k] = 0u;
-      }
+      chains_scan<U>(lds, lb, wd, lane, raw, pre, cp);
     } else {  // the range's single-chunk units
-      uint32_t wd[1][16], l1[1], r1[1], f1[1] = {Lf[0]}, q1[1], c1[1][3];
+      uint32_t wd[1][16], r1[1], p1[1], c1[1][3];
 #pragma unroll
       for (int q = 0; q < 16; ++q) wd[0][q] = cur[0].d[q];
       row_transpose(wd[0]);
-      chains_first<1>(lds, lb, wd, lane, f1, l1, r1, q1, c1);
+      chains_scan<1>(lds, lb, wd, lane, r1, p1, c1);
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        lr[k] = l1[0];
         raw[k] = r1[0];
-        qf[k] = q1[0];
+        pre[k] = p1[0];
 #pragma unroll
         for (int m = 0; m < 3; ++m) cp[k][m] = c1[0][m];
       }
@@ -3132,7 +3136,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     // (a unit with no event and no buffer running past its window -- most of
     // config 3's -- has nothing to record)
     if (any_ev || (cursor + 64u < g.n && lane_u64(w.s, 63) < (ca + cu) * kChunk))
-      region_events<U>(g, lds, w, cursor, ca, cu, lr, Lf, qf, cp, le, lane);
+      region_events<U>(g, w, cursor, ca, cu, pre, Lf, cp, le, lane);
 
     u = un;
     ca = can;
@@ -3146,7 +3150,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
 }
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRLdsBytes];
   run_region<NVL_FAST_U>(g, ka, lds);
 }
 

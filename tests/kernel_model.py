@@ -425,6 +425,32 @@ def masked_fold(lane_raws, L: int) -> int:
     return wave_fold([v if l < L else 0 for l, v in enumerate(lane_raws)])
 
 
+def nibble_table(n: int, v: int, j: int) -> int:
+    """The region kernel's LDS nibble tables: T[n][v][j] = shift(v << 4n, 64(63 - j))."""
+    return shift(v << (4 * n), 64 * (63 - j))
+
+
+def lane_scan(lane_raws):
+    """crc32c_region_kernel's chunk_scan: each lane moves its piece raw to the
+    chunk end through its nibble-table column (lane 63: identity), then an
+    inclusive XOR scan over lanes.  Returns (chunk raw, exclusive prefixes):
+    pre[L] = Qe(L) = masked_fold(lane_raws, L)."""
+    t = []
+    for j, v in enumerate(lane_raws):
+        if j == 63:
+            t.append(v)
+            continue
+        acc = 0
+        for n in range(8):
+            acc ^= nibble_table(n, (v >> (4 * n)) & 15, j)
+        t.append(acc)
+    inc, acc = [], 0
+    for x in t:
+        acc ^= x
+        inc.append(acc)
+    return inc[63], [i ^ x for i, x in zip(inc, t)]
+
+
 def region_events(s: int, e: int, L: int):
     """The (chunk, in-chunk offset) events a buffer [s, e) leaves for the
     chunk kernel: its start unless on a chunk boundary, its end unless on one."""
@@ -484,19 +510,20 @@ def unshift(v: int, nbytes: int) -> int:
 
 
 def region_batch(mem: bytes, bufs, inits):
-    """Every buffer of a region batch through the model: chunk pass (raws,
-    per-lane raws, Qe at each event's lane), then the per-buffer fold."""
+    """Every buffer of a region batch through the model: chunk pass (raws and
+    lane prefixes by lane_scan, Qe = the prefix at each event's lane), then
+    the per-buffer fold."""
     NC = (len(mem) + 4095) // 4096
     mem = mem + bytes(NC * 4096 - len(mem))
-    raws, lanes = [], []
+    raws, pres = [], []
     for c in range(NC):
-        lr = piece_raws(mem[4096 * c:4096 * c + 4096])
-        lanes.append(lr)
-        raws.append(wave_fold(lr))
+        raw, pre = lane_scan(piece_raws(mem[4096 * c:4096 * c + 4096]))
+        raws.append(raw)
+        pres.append(pre)
     qe = {}
     for s, L in bufs:
         for kind, c, o in region_events(s, s + L, L):
-            qe[(kind, c, o)] = masked_fold(lanes[c], o >> 6)
+            qe[(kind, c, o)] = pres[c][o >> 6]
     return [region_fold(mem, raws, qe, s, L, i) for (s, L), i in zip(bufs, inits)]
 
 

@@ -207,6 +207,20 @@ def test_region_path_model(port, seed):
     assert got == want
 
 
+def test_region_lane_scan(port):
+    """The region kernel's chunk step: per-lane nibble-table shifts to the
+    chunk end + XOR scan give the chunk raw and, at every lane L, the masked
+    butterfly Qe(L) (the chunk bytes [0, 64L) at the chunk end)."""
+    rng = random.Random(21)
+    for _ in range(3):
+        chunk = bytes(rng.getrandbits(8) for _ in range(4096))
+        lr = km.piece_raws(chunk)
+        raw, pre = km.lane_scan(lr)
+        assert raw == km.raw_bytes(0, chunk) == km.wave_fold(lr)
+        for L in range(64):
+            assert pre[L] == km.masked_fold(lr, L), L
+
+
 def test_region_quad_prefix_from_checkpoints(port):
     """The fold kernel's R(p) from the chunk kernel's chain checkpoint and one
     16-byte quad equals the piece prefix's raw at every offset 0..63."""

@@ -24,7 +24,9 @@ sed -e 's|^  const uint64_t co = ldg64(g.offsets, ci), cl = ldg64(g.lengths, ci)
     -e 's|^    for (uint64_t i = i0 + 64u + (uint64_t)lane; i < i1; i += 64u) {  // slices of more than 64 buffers|    for (uint64_t i = i1; i < i1; i += 64u) {|' \
     $R/build/abl_rnowin.hip > $R/build/abl_rbare.hip
 [ $(grep -c 'const uint64_t co = 0, cl = 0;\|const uint64_t po = 0, pl = 0;\|for (uint64_t i = i1; i < i1;' $R/build/abl_rbare.hip) -eq 3 ] || { echo "rbare: anchors" >&2; exit 1; }
-for v in rnoev rnowin rnofold rbare; do
+#   rpure    rbare without the fold kernel: the chunk pass alone
+sed -e 's|^  dev::RegionFold f{|  return hipGetLastError();\n  dev::RegionFold f{|' $R/build/abl_rbare.hip > $R/build/abl_rpure.hip
+for v in rnoev rnowin rnofold rbare rpure; do
   make -C $R/nvlevelz_amd/csrc variant NAME=$v VSRC=$R/build/abl_$v.hip VFLAGS="-I$R/nvlevelz_amd/csrc" > /dev/null
 done
-echo built build/libnvl_crc32c_{rnoev,rnowin,rnofold,rbare}.so
+echo built build/libnvl_crc32c_{rnoev,rnowin,rnofold,rbare,rpure}.so

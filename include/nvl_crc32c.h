@@ -164,7 +164,7 @@ NVL_API int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len,
                                         uint32_t* out, uint64_t n, uint32_t flags, void* workspace,
                                         size_t workspace_bytes, void* stream, void* start_event, void* stop_event);
 
-/* Workspace bytes nvl_crc32c_region_dev needs (4 B per 4 KiB of region + 8 B per buffer). */
+/* Workspace bytes nvl_crc32c_region_dev needs (4 B per 4 KiB of region + 32 B per buffer). */
 NVL_API size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n);
 
 /* ---- batched, host-resident (end-to-end path) ---------------------------- */

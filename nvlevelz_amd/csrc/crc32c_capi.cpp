@@ -39,7 +39,7 @@ void build_device_tables(uint32_t* w) {
   // in the reflected form is v >> 1 (^ P when bit 0 = x^31 overflows); its
   // inverse: bit 31 (x^0) set means P was added, so v = ((v ^ P) << 1) | 1.
   uint32_t p = kOne, q = kOne;
-  for (uint32_t d = 0; d <= 4096; ++d) {
+  for (uint32_t d = 0; d < kXp8Len; ++d) {
     w[kTabXp8 + d] = p;
     if (d < 4096) w[kTabXm8 + d] = q;
     for (int b = 0; b < 8; ++b) {
@@ -286,8 +286,6 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
 }
 
 // Region batch: page-aligned chunk pass + per-buffer fold (launch_region).
-// Needs the stream's counter block; without one (more than
-// kMaxCounterStreams streams) the batch runs through do_batch instead.
 int do_region(DeviceState* s, const void* region, uint64_t region_len, const uint64_t* offsets,
               const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
               uint32_t flags, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t ev_start = nullptr,
@@ -295,8 +293,7 @@ int do_region(DeviceState* s, const void* region, uint64_t region_len, const uin
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out || !region) return NVL_CRC32C_EINVAL;
   if (n >= (1ull << 31) - 2 || region_len > (1ull << 50)) return NVL_CRC32C_EINVAL;
-  LaunchCtx lc{st, s->num_cu, s->tables, counters_for(s, st), ev_start, ev_stop};
-  if (!lc.counter) return do_batch(s, region, offsets, lengths, init, init_all, out, n, flags, nullptr, 0, st);
+  LaunchCtx lc{st, s->num_cu, s->tables, nullptr, ev_start, ev_stop};
   const size_t need = region_ws_bytes(region_len, n);
   bool own = false;
   if (!ws) {

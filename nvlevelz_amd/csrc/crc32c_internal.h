@@ -17,12 +17,13 @@ namespace nvl {
 //   [1024,  7168)  comb[6][4][256]    shift by 64*2^k bytes, byte-sliced
 //   [7168,  8192)  sh4096[4][256]     shift by 4096 bytes, byte-sliced
 //   [8192,  8256)  x2n[64]            x^(2^k) mod P
-//   [8256, 12353)  xp8[4097]          x^(8d) mod P, d = 0..4096        (region fold)
-//   [12353,16449)  xm8[4096]          x^(-8d) mod P, d = 0..4095       (region fold)
-//   [16452,24644)  nib[8][16][64]     T[n][v][j] = shift(v << 4n, 64(63 - j))  (region kernel:
+//   [8256, 16449)  xp8[8193]          x^(8d) mod P, d = 0..8192        (region fold)
+//   [16449,20545)  xm8[4096]          x^(-8d) mod P, d = 0..4095       (region fold)
+//   [20548,28740)  nib[8][16][64]     T[n][v][j] = shift(v << 4n, 64(63 - j))  (region kernel:
 //                                     lane j's piece raw to the chunk end; 16-byte aligned, copied
 //                                     verbatim into LDS)
-constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + 4097;
+constexpr uint32_t kXp8Len = 8193;  // a buffer spanning at most two chunks has at most 8192 bytes
+constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + kXp8Len;
 constexpr uint32_t kTabNib = (kTabXm8 + 4096u + 3u) & ~3u;
 constexpr uint32_t kTableWords = kTabNib + 8u * 16u * 64u;
 
@@ -94,14 +95,12 @@ bool var_heads_only(int num_cu, uint64_t n, uint64_t max_len);
 
 // Region batch (nvl_crc32c_region_dev): n buffers inside [region, region +
 // region_len), checksummed over the region's page-aligned 4 KiB chunks and
-// folded per buffer.  ws: region_ws_bytes(region_len, n).  counter: the
-// stream's counter block (words kRegionFlag / kRegionDone).
+// folded per buffer in the same launch.  ws: region_ws_bytes(region_len, n)
+// (chunk raws and gen-tagged event records; never needs resetting).
 size_t region_ws_bytes(uint64_t region_len, uint64_t n);
 hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* ws);
-constexpr uint32_t kRegionFlag = 16;  // counter-block word (the fused kernel uses word 0): the generation of
-                                      // the last region call whose batch was not region-shaped
 
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

@@ -894,6 +894,9 @@ __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane, uint32_t c
 #define NVL_TL(k) do {} while (0)
 #define NVL_TL_END() do {} while (0)
 #endif
+#ifndef NVL_TL_WAIT  // NVL_TL(k) once the wave's loads (and value v) are in
+#define NVL_TL_WAIT(k, v) do {} while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // Scheduler A -- fixed stride, aligned, J == 1 (every chunk a whole buffer;
@@ -2740,11 +2743,12 @@ struct RegionGeom {
   const uint64_t* offsets;  // from the region start
   const uint64_t* lengths;
   uint64_t n;
+  const uint32_t* init;  // per-buffer Extend seeds (nullptr: init_all)
+  uint32_t init_all;
   uint32_t* raws;  // [nc]
-  uint2* qs;       // [n] buffer i's start event: {Qe, lane L's chain checkpoint x_4c}
-  uint2* qe;       // [n] its end event
-  uint32_t* ctr;   // the stream's counter block
-  uint32_t gen;    // this call's generation: ctr[kRegionFlag] = gen marks the batch as not region-shaped
+  uint4* qs;       // [n] buffer i's start event: {Qe, lane L's chain checkpoint x_4c, gen, 0}
+  uint4* qe;       // [n] its end event
+  uint32_t gen;    // this call's generation: a record without it was not written by this call
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* g64_ptr;
@@ -2776,16 +2780,28 @@ __device__ __forceinline__ Win make_win(const RegionGeom& g, const WinRaw& r, ui
 }
 
 // First buffer b with e_b > A (n when none), for non-decreasing ends: a
-// 64-ary search, one wave-wide load per level.
-__device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane) {
+// 64-ary search, one wave-wide load per level.  The first level, a window at
+// the interpolated index (a packed region of similar buffers: the answer),
+// is loaded by region_probe so that the caller can issue it early.
+struct SearchProbe {
+  uint64_t w0, e;
+};
+__device__ __forceinline__ SearchProbe region_probe(const RegionGeom& g, uint64_t A, int lane) {
+  const double f = (double)A / (double)(g.rel0 + g.region_len + 1u);
+  const uint64_t gi = min((uint64_t)(f * (double)g.n), g.n - 1u);
+  const uint64_t w0 = gi > 32u ? gi - 32u : 0u;
+  const uint64_t b = min(w0 + (uint64_t)lane, g.n - 1u);
+  return SearchProbe{w0, g.rel0 + ldg64(g.offsets, b) + ldg64(g.lengths, b)};
+}
+__device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane, const SearchProbe& p);
+__device__ __forceinline__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane) {
+  return region_search(g, A, lane, region_probe(g, A, lane));
+}
+__device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane, const SearchProbe& p) {
   uint64_t lo = 0, hi = g.n;  // every b < lo has e_b <= A; the answer is <= hi
-  {  // first a window at the interpolated index (a packed region of similar buffers: one load)
-    const double f = (double)A / (double)(g.rel0 + g.region_len + 1u);
-    const uint64_t gi = min((uint64_t)(f * (double)g.n), g.n - 1u);
-    const uint64_t w0 = gi > 32u ? gi - 32u : 0u;
-    const uint64_t b = min(w0 + (uint64_t)lane, g.n - 1u);
-    const uint64_t e = g.rel0 + ldg64(g.offsets, b) + ldg64(g.lengths, b);
-    const uint64_t m = __ballot(w0 + (uint64_t)lane < g.n && e > A);
+  {
+    const uint64_t w0 = p.w0;
+    const uint64_t m = __ballot(w0 + (uint64_t)lane < g.n && p.e > A);
     if (m & 1u) {
       if (w0 == 0) return 0;
       hi = w0;  // the answer lies below the window
@@ -2831,29 +2847,44 @@ static_assert(kRLdsBytes <= 160u * 1024u, "region LDS image exceeds 160 KiB");
 constexpr uint32_t kGNib = kTabNib;  // the blob's nibble tables (crc32c_internal.h)
 
 // The region image: slice replicas at kRSliceOff, nibble tables verbatim,
-// the unit counter patched into its slot by the thread that copies it.
-template <int NW>
-__device__ __forceinline__ void fill_lds_region(uint8_t* lds, const uint32_t* __restrict__ g, uint32_t ctr0) {
-  constexpr int kT = kWave * NW;
+// the unit counter patched into its slot by the thread that copies it.  In
+// two halves so that the blob loads are in flight together with the waves'
+// first searches (a fill after the search waited for both in turn: 6 us to
+// the first barrier).
+struct RegionFill {
+  uint32_t rep[8192 / kThreads];
+  uint4 nib[2048 / kThreads];
+};
+__device__ __forceinline__ RegionFill fill_region_load(const uint32_t* __restrict__ g) {
+  RegionFill f;
   const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < (8192 + kT - 1) / kT; ++q) {
-    const uint32_t s = (uint32_t)(t + q * kT);
-    if ((8192 % kT) != 0 && s >= 8192u) break;
-    const uint32_t off = s << 4;
+  for (int q = 0; q < (int)(8192 / kThreads); ++q) {
+    const uint32_t off = (uint32_t)(t + q * (int)kThreads) << 4;
     const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
-    const uint32_t b = (off >> 8) & 0xFFu;
-    const uint32_t v = g[kGSlice + tab * 256u + b];
-    *reinterpret_cast<uint4*>(lds + kRSliceOff + off) = make_uint4(v, v, v, v);
+    f.rep[q] = g[kGSlice + tab * 256u + ((off >> 8) & 0xFFu)];
   }
   const uint4* src = reinterpret_cast<const uint4*>(g + kGNib);
+#pragma unroll
+  for (int q = 0; q < (int)(2048 / kThreads); ++q) f.nib[q] = src[t + q * (int)kThreads];
+  return f;
+}
+__device__ __forceinline__ void fill_region_store(uint8_t* lds, const RegionFill& f, uint32_t ctr0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < (int)(8192 / kThreads); ++q) {
+    const uint32_t off = (uint32_t)(t + q * (int)kThreads) << 4;
+    *reinterpret_cast<uint4*>(lds + kRSliceOff + off) = make_uint4(f.rep[q], f.rep[q], f.rep[q], f.rep[q]);
+  }
   uint4* dst = reinterpret_cast<uint4*>(lds + kRNibOff);
-  for (int q = t; q < 2048; q += kT) {
-    uint4 v = src[q];
-    if (q == (int)(kRCtrOff >> 4)) v.w = ctr0;  // units 0..ctr0-1 are pre-assigned
-    dst[q] = v;
+#pragma unroll
+  for (int q = 0; q < (int)(2048 / kThreads); ++q) {
+    uint4 v = f.nib[q];
+    if (t + q * (int)kThreads == (int)(kRCtrOff >> 4)) v.w = ctr0;  // units 0..ctr0-1 are pre-assigned
+    dst[t + q * (int)kThreads] = v;
   }
 }
+static_assert(8192 % kThreads == 0 && 2048 % kThreads == 0, "region fill: whole rounds per thread");
 
 // shift(lr, 64(63 - lane)): this lane's piece raw moved to the chunk end.
 // Address of row (n, v): v << 8 | lane << 2 -- v_perm puts the nibble byte
@@ -2990,8 +3021,8 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, Win w, uint64
   for (;;) {
     uint2 rs, re;
     const bool fs = le.sv && rec(le.ps, rs), fe = le.ev && rec(le.pe, re);
-    if (fs) g.qs[cur + (uint64_t)lane] = rs;
-    if (fe) g.qe[cur + (uint64_t)lane] = re;
+    if (fs) g.qs[cur + (uint64_t)lane] = make_uint4(rs.x, rs.y, g.gen, 0u);
+    if (fe) g.qe[cur + (uint64_t)lane] = make_uint4(re.x, re.y, g.gen, 0u);
     const uint64_t ms = __ballot(le.sv && !fs), me = __ballot(le.ev && !fe);
     uint64_t all = ms | me;
     while (all) {  // events on another lane than their chunk's first
@@ -3009,7 +3040,7 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, Win w, uint64
 #pragma unroll
           for (int m = 0; m < 3; ++m) x = (k == (uint32_t)q && c == (uint32_t)m + 1u) ? cp[q][m] : x;
         }
-        const uint2 r = make_uint2(lane_u32(v, L), lane_u32(x, L));
+        const uint4 r = make_uint4(lane_u32(v, L), lane_u32(x, L), g.gen, 0u);
         if (lane == 0) (t ? g.qe : g.qs)[cur + j] = r;
       }
     }
@@ -3019,158 +3050,6 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, Win w, uint64
     le = lane_events(w, A, B);
   }
 }
-
-// Scheduler A over the region's chunks: the workgroup owns a contiguous
-// chunk range, its waves pull 2-chunk units from an LDS counter, the next
-// unit's chunks and metadata window are in flight while this one computes.
-template <int U>
-__device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
-  const uint64_t B0 = g.nc * blockIdx.x / gridDim.x;
-  const uint64_t B1 = g.nc * (blockIdx.x + 1) / gridDim.x;
-  const uint32_t cnt = (uint32_t)(B1 - B0);
-  const uint32_t nfull = cnt > kTail ? (cnt - kTail) / U : 0u;
-  const uint32_t nunits = nfull + (cnt - nfull * U);
-  auto first_of = [&](uint32_t u) -> uint64_t {
-    return u < nfull ? B0 + (uint64_t)u * U : B0 + (uint64_t)nfull * U + (u - nfull);
-  };
-  auto count_of = [&](uint32_t u) -> uint32_t { return u >= nunits ? 0u : (u < nfull ? (uint32_t)U : 1u); };
-  auto load_unit = [&](uint64_t ca, uint32_t cu, Chunk (&ch)[U]) {
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      if ((uint32_t)k < cu) {
-        const uintptr_t cs = (uintptr_t)g.grid + (ca + (uint64_t)k) * kChunk;
-        const uint32_t lo = lane_load_off(lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const u32x4 v = ld16(cs + 1024u * (uint32_t)j + lo);
-          ch[k].d[4 * j + 0] = v.x; ch[k].d[4 * j + 1] = v.y; ch[k].d[4 * j + 2] = v.z; ch[k].d[4 * j + 3] = v.w;
-        }
-      }
-    }
-  };
-
-  uint32_t u = wv;  // first unit pre-assigned: its loads overlap the search and the LDS fill
-  uint64_t ca = first_of(u);
-  uint32_t cu = count_of(u);
-  Chunk cur[U];
-  load_unit(ca, cu, cur);
-  uint64_t cursor = cu ? region_search(g, ca * kChunk, lane) : g.n;
-  WinRaw wr = load_win(g, cursor, lane);
-  // The batch check (sorted by offset, non-overlapping, inside the region),
-  // one slice per wave: the first 64 buffers' loads go out before the LDS
-  // fill so their latency hides behind it (a check after the units delayed
-  // the last wave's end).
-  const uint64_t per = (g.n + (uint64_t)gridDim.x * kWavesPerWG - 1u) / ((uint64_t)gridDim.x * kWavesPerWG);
-  const uint64_t i0 = min(g.n, ((uint64_t)blockIdx.x * kWavesPerWG + wv) * per), i1 = min(g.n, i0 + per);
-  const uint64_t ci = min(i0 + (uint64_t)lane, g.n - 1u), cp = ci ? ci - 1u : 0u;
-  const uint64_t co = ldg64(g.offsets, ci), cl = ldg64(g.lengths, ci);
-  const uint64_t po = ldg64(g.offsets, cp), pl = ldg64(g.lengths, cp);
-  fill_lds_region<kWavesPerWG>(lds, ka.tables, kWavesPerWG);
-  __syncthreads();
-  {
-    bool bad = false;
-    if (i0 + (uint64_t)lane < i1) {
-      bad = co > g.region_len || cl > g.region_len - co;
-      if (ci > 0) bad |= co < po + pl;
-    }
-    for (uint64_t i = i0 + 64u + (uint64_t)lane; i < i1; i += 64u) {  // slices of more than 64 buffers
-      const uint64_t o = ldg64(g.offsets, i), L = ldg64(g.lengths, i);
-      bad |= o > g.region_len || L > g.region_len - o;
-      bad |= o < ldg64(g.offsets, i - 1) + ldg64(g.lengths, i - 1);
-    }
-    if (__ballot(bad) && lane == 0) g.ctr[kRegionFlag] = g.gen;
-  }
-  const LaneBase lb = make_lane_base(lane);
-
-  while (u < nunits) {
-    const uint32_t un = pull_unit(lds, lane, kRCtrOff);
-    const Win w = make_win(g, wr, cursor, lane);
-    const uint64_t can = first_of(un);
-    const uint32_t cun = count_of(un);
-    uint64_t ncur = g.n;
-    if (cun) {  // the next unit's cursor: the first buffer of this window ending after its start
-      const uint64_t m = __ballot(w.valid && w.e > can * kChunk);
-      ncur = m ? cursor + (uint64_t)__builtin_ctzll(m) : min(cursor + 64u, g.n);
-    }
-    const WinRaw nwr = load_win(g, ncur, lane);
-    Chunk nxt[U];
-    load_unit(can, cun, nxt);
-
-    const LaneEv le = lane_events(w, ca * kChunk, (ca + cu) * kChunk);
-    const bool any_ev = __ballot(le.sv || le.ev) != 0u;
-    uint32_t Lf[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) Lf[k] = 0u;
-    if (any_ev) first_lanes<U>(le, Lf);
-    uint32_t raw[U], pre[U], cp[U][3];
-    if (cu == (uint32_t)U) {
-      uint32_t wd[U][16];
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
-        row_transpose(wd[k]);
-      }
-      chains_scan<U>(lds, lb, wd, lane, raw, pre, cp);
-    } else {  // the range's single-chunk units
-      uint32_t wd[1][16], r1[1], p1[1], c1[1][3];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) wd[0][q] = cur[0].d[q];
-      row_transpose(wd[0]);
-      chains_scan<1>(lds, lb, wd, lane, r1, p1, c1);
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        raw[k] = r1[0];
-        pre[k] = p1[0];
-#pragma unroll
-        for (int m = 0; m < 3; ++m) cp[k][m] = c1[0][m];
-      }
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
-    }
-    // (a unit with no event and no buffer running past its window -- most of
-    // config 3's -- has nothing to record)
-    if (any_ev || (cursor + 64u < g.n && lane_u64(w.s, 63) < (ca + cu) * kChunk))
-      region_events<U>(g, w, cursor, ca, cu, pre, Lf, cp, le, lane);
-
-    u = un;
-    ca = can;
-    cu = cun;
-    cursor = ncur;
-    wr = nwr;
-#pragma unroll
-    for (int k = 0; k < U; ++k) cur[k] = nxt[k];
-  }
-
-}
-
-__global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRLdsBytes];
-  run_region<NVL_FAST_U>(g, ka, lds);
-}
-
-// Per-buffer fold of a region batch (one thread per buffer).
-struct RegionFold {
-  const uint8_t* grid;
-  uint64_t rel0;
-  const uint64_t* offsets;
-  const uint64_t* lengths;
-  uint64_t n;
-  const uint32_t* init;
-  uint32_t init_all, flags;
-  const uint32_t* raws;
-  const uint2* qs;
-  const uint2* qe;
-  const uint32_t* tables;
-  uint32_t* out;
-  const uint32_t* ctr;
-  uint32_t gen;
-};
 
 __device__ __forceinline__ uint32_t fold_slice4(const uint32_t* t, uint32_t x) {
   return t[768u + (x & 255u)] ^ t[512u + ((x >> 8) & 255u)] ^ t[256u + ((x >> 16) & 255u)] ^ t[x >> 24];
@@ -3222,59 +3101,419 @@ __device__ __forceinline__ uint32_t fold_sh4096(const uint32_t* sh, uint32_t acc
   return sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)];
 }
 
-__global__ __launch_bounds__(256) void crc32c_region_fold_kernel(RegionFold a) {
-  __shared__ uint32_t sl[1024];  // slice4 t[k][b] (util/crc32c.cc table0_..table3_)
-  __shared__ uint32_t sh[1024];  // shift by 4096 bytes, byte-sliced
-  for (uint32_t t = threadIdx.x; t < 1024u; t += blockDim.x) {
-    sl[t] = a.tables[kGSlice + t];
-    sh[t] = a.tables[kGComb + 6u * 1024u + t];
+// The fold of one region buffer, in two halves.  fold_in: what depends on
+// the batch alone -- its metadata, the two 16-byte quads re-read for the
+// piece prefixes R (the end's clamped into the grid when it is a chunk end),
+// the powers -- issued before the workgroup's last unit is done.  fold_out:
+// the chunk raws and gen-tagged event records this workgroup wrote (after
+// its barrier), then the arithmetic; false when a record is missing (not
+// written by this call: the batch was not region-shaped there) -- the
+// caller then checksums the buffer serially.
+struct FoldIn {
+  uint64_t s, L;
+  uint32_t ninit, xs, xe, xo, xl;  // x^(8(4096 - os)), x^(-8(4096 - oe)), x^(8 oe), x^(8L) (L < 8192)
+  u32x4 vs, ve;
+  bool fast;  // inside the region, >= kRegionDirect bytes, every chunk streamed by this workgroup
+};
+__device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* tables, uint64_t i, uint64_t c0w,
+                                          uint64_t B1) {
+  FoldIn f;
+  const uint64_t off = ldg64(g.offsets, i), L = ldg64(g.lengths, i);
+  f.ninit = ~(g.init ? g.init[i] : g.init_all);
+  f.s = g.rel0 + off;
+  f.L = L;
+  const bool inside = off <= g.region_len && L <= g.region_len - off;
+  f.fast = inside && L >= kRegionDirect && (f.s >> 12) >= c0w && ((f.s + L - 1u) >> 12) < B1;
+  const uint64_t s = f.fast ? f.s : 0u, e = f.fast ? f.s + L : 64u;  // (the grid's first chunk otherwise)
+  const uint64_t c1 = (e - 1u) >> 12;
+  const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
+  f.vs = ld16c((uintptr_t)g.grid + (s & ~(uint64_t)15));
+  f.ve = ld16c((uintptr_t)g.grid + (oe == kChunk ? e - 16u : (e & ~(uint64_t)15)));
+  f.xs = tables[kTabXp8 + kChunk - os];
+  f.xe = tables[kTabXm8 + (kChunk - oe)];
+  f.xo = tables[kTabXp8 + oe];
+  f.xl = tables[kTabXp8 + min(e - s, (uint64_t)kXp8Len - 1u)];
+  return f;
+}
+
+// quad_prefix over the LDS slice replicas (lsl, lb: as the chains).
+__device__ __forceinline__ uint32_t quad_prefix_lds(const uint8_t* lsl, const LaneBase& lb, uint32_t x, const u32x4& v,
+                                                    uint32_t o) {
+  const uint32_t c = o >> 4, m = (o >> 2) & 3u, r = o & 3u;
+  uint32_t crc = c ? x ^ v[0] : 0u, cur = v[0];
+#pragma unroll
+  for (uint32_t j = 0; j < 3u; ++j) {
+    const uint32_t nx = slice4(lsl, crc ^ v[j], lb);
+    crc = j < m ? nx : crc;
+    cur = j + 1u == m ? v[j + 1u] : cur;
   }
-  // the chunk kernel of THIS call found the batch out of order (a flag left
-  // by an earlier call carries another generation: nothing is ever reset)
-  const bool bad = ldc(a.ctr, kRegionFlag) == a.gen;
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.n) {
-    const uint64_t off = a.offsets[i], L = a.lengths[i];
-    const uint32_t ninit = ~(a.init ? a.init[i] : a.init_all);
-    const uint64_t s = a.rel0 + off;
-    uint32_t v;
-    if (bad || L < kRegionDirect) {
-      v = serial_raw(sl, ninit, a.grid + s, L);
-    } else {
-      const uint64_t e = s + L;
-      const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
-      const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
-      // every load first: the two events' quads (the end's clamped into the
-      // grid when it is a chunk end) and records, the end chunks' raws, the powers
-      const uintptr_t gs = (uintptr_t)a.grid + (s & ~(uint64_t)15);
-      const uintptr_t ge = (uintptr_t)a.grid + (oe == kChunk ? e - 16u : (e & ~(uint64_t)15));
-      const u32x4 vs = ld16c(gs), ve = ld16c(ge);
-      const uint2 q_s = a.qs[i], q_e = a.qe[i];
-      const uint32_t r0 = a.raws[c0], r1 = a.raws[c1];
-      const uint32_t xs = a.tables[kTabXp8 + kChunk - os], xe = a.tables[kTabXm8 + (kChunk - oe)];
-      // Ze'(s) = Qe(s) ^ (R(s) ^ ~init) x^(8(4096 - os)): bytes [cs0, s) and ~init at s, at the chunk end
-      const uint32_t zs = (os ? q_s.x : 0u) ^ gf_mul(xs, (os ? quad_prefix(sl, q_s.y, vs, s & 63u) : 0u) ^ ninit);
-      uint32_t acc = zs;
-      if (c0 != c1) {
-        acc ^= r0;
-        for (uint64_t c = c0 + 1u; c < c1; c += 4u) {  // the chunks in between, four loads at a time
-          uint32_t rr[4];
+  const uint8_t* sl = lsl + kSliceOff;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) rr[k] = a.raws[min(c + (uint64_t)k, c1)];
+  for (uint32_t b = 0; b < 3u; ++b) {  // T0[(crc ^ byte) & 255] ^ crc >> 8 (table 0 = byte 3's slot of slice4)
+    const uint32_t nx = lds_u32(sl, __builtin_amdgcn_perm(crc ^ (cur >> (8u * b)), lb.t0, 0x0C020400u)) ^ (crc >> 8);
+    crc = b < r ? nx : crc;
+  }
+  return crc;
+}
+
+// gf_mul(a, b) (crc32c_math.h) by bytes of a, Horner in x^8: with
+// B_j = b x^j (j < 8), C_k = sum_j a_{8k+j} B_j, a b = C_0 ^ x^8 (C_1 ^ x^8 (C_2
+// ^ x^8 C_3)), and v x^8 = T0[v & 255] ^ v >> 8 -- one LDS lookup (slice
+// table 0's replica) per byte instead of eight shift-reduce steps.  Bit
+// 31 - i of a is its x^i coefficient (reflected).
+__device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* lsl, const LaneBase& lb, uint32_t a, uint32_t b) {
+  uint32_t B[8];
+  B[0] = b;
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (c + (uint64_t)k < c1) acc = fold_sh4096(sh, acc) ^ rr[k];
-        }
-        acc = fold_sh4096(sh, acc);
+  for (int j = 1; j < 8; ++j)
+    B[j] = (B[j - 1] >> 1) ^ ((uint32_t)__builtin_amdgcn_sbfe((int)B[j - 1], 0, 1) & kPolyReflected);
+  const uint8_t* sl = lsl + kSliceOff;
+  uint32_t p = 0u;
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {
+    if (k < 3) p = lds_u32(sl, __builtin_amdgcn_perm(p, lb.t0, 0x0C020400u)) ^ (p >> 8);  // p x^8
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p ^= (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - (8 * k + j), 1) & B[j];
+  }
+  return p;
+}
+
+// shift(v, 64 (63 - j)) through column j of the nibble tables (jb = 4j).
+__device__ __forceinline__ uint32_t col_shift(const uint8_t* lds, uint32_t v, uint32_t jb) {
+  const uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
+  const uint8_t* nb = lds + kRNibOff;
+  const uint32_t r0 = lds_u32(nb + 0u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0400u));
+  const uint32_t r1 = lds_u32(nb + 1u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0400u));
+  const uint32_t r2 = lds_u32(nb + 2u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0500u));
+  const uint32_t r3 = lds_u32(nb + 3u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0500u));
+  const uint32_t r4 = lds_u32(nb + 4u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0600u));
+  const uint32_t r5 = lds_u32(nb + 5u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0600u));
+  const uint32_t r6 = lds_u32(nb + 6u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0700u));
+  const uint32_t r7 = lds_u32(nb + 7u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0700u));
+  return xor3(xor3(r0, r1, r2), xor3(r3, r4, r5), r6) ^ r7;
+}
+
+// shift(acc, 4096) as two column shifts, 64 a and 64 (64 - a) bytes with
+// a = (lane & 31) + 1: the 32 lanes of a half read 32 distinct columns
+// (banks) -- one shared column would serialise them.
+__device__ __forceinline__ uint32_t sh4096_lds(const uint8_t* lds, uint32_t acc, int lane) {
+  const uint32_t a = ((uint32_t)lane & 31u) + 1u;
+  return col_shift(lds, col_shift(lds, acc, (63u - a) << 2), (a - 1u) << 2);
+}
+
+__device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds, const uint8_t* lsl,
+                                         const LaneBase& lb, int lane, const FoldIn& f, const uint4& q_s,
+                                         const uint4& q_e, uint32_t& v) {
+  const uint64_t s = f.s, e = f.s + f.L;
+  const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
+  const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
+  const uint32_t r0 = g.raws[c0], r1 = g.raws[c1], rm = g.raws[min(c0 + 1u, c1)];
+  if ((os && q_s.z != g.gen) || (oe != kChunk && q_e.z != g.gen)) return false;
+  const uint32_t qs = os ? q_s.x : 0u;                                   // chunk c0's bytes before s, at its end
+  const uint32_t T = (os ? quad_prefix_lds(lsl, lb, q_s.y, f.vs, s & 63u) : 0u) ^ f.ninit;  // R(s) ^ ~init, at s
+  const uint32_t ze = oe == kChunk ? r1 : q_e.x;                         // chunk c1's bytes before e, at its end
+  const uint32_t re = oe == kChunk ? 0u : quad_prefix_lds(lsl, lb, q_e.y, f.ve, e & 63u);  // R(e), at e
+  if (c1 <= c0 + 1u) {
+    // Everything moved straight to e, three independent multiplies:
+    //   c1 = c0 + 1: (Qe(s) ^ raw c0) x^(8 oe) ^ T x^(8L) ^ Ze x^(-8(4096 - oe)) ^ R(e)
+    //   c1 = c0:     (Ze ^ Qe(s)) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e)
+    const bool two = c1 != c0;
+    v = gf_mul_lds(lsl, lb, f.xo, two ? qs ^ r0 : 0u) ^ gf_mul_lds(lsl, lb, f.xl, T) ^
+        gf_mul_lds(lsl, lb, f.xe, two ? ze : ze ^ qs) ^ re;
+    return true;
+  }
+  // Longer: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) at chunk c0's end, the chunks in between, unshifted from c1's end
+  uint32_t acc = qs ^ gf_mul_lds(lsl, lb, f.xs, T) ^ r0;
+  acc = sh4096_lds(lds, acc, lane) ^ rm;
+  for (uint64_t c = c0 + 2u; c < c1; c += 4u) {  // further chunks in between, four loads at a time
+    uint32_t rr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rr[k] = g.raws[min(c + (uint64_t)k, c1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + (uint64_t)k < c1) acc = sh4096_lds(lds, acc, lane) ^ rr[k];
+  }
+  acc = sh4096_lds(lds, acc, lane);
+  v = gf_mul_lds(lsl, lb, f.xe, acc ^ ze) ^ re;
+  return true;
+}
+
+// LDS slots in the region image's lane-63 column (never read by the lane
+// shifts): row r at r * 256 + 252.  Row 16 (T[1][0][63]) is 0 in the blob.
+// (an LDS-qualified pointer: through a generic one the volatile accesses
+// became flat loads, which count in vmcnt -- every wait on them was a
+// vmcnt(0) that also waited for the next unit's chunks)
+typedef volatile __attribute__((address_space(3))) uint32_t lds_vu32;
+__device__ __forceinline__ lds_vu32* region_slot(uint8_t* lds, uint32_t r) {
+  return (lds_vu32*)(lds + kRNibOff + r * 256u + 252u);
+}
+constexpr uint32_t kSlotOwnLo = 1, kSlotOwnHi = 2, kSlotEndLo = 3, kSlotEndHi = 4, kSlotHalo = 5;
+constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32: T[1][0][63], T[2][0][63] = 0 in the blob)
+
+// Scheduler A over the region's chunks, and the per-buffer fold in the same
+// launch.  Workgroup b owns the chunk range [B0, B1) and the buffers
+// [I_b, I_b+1), I_b = the first buffer ending after chunk B0's start (I_0 = 0,
+// I_G = n): every buffer's end event lies in its owner's range.  The one
+// owned buffer that starts in an earlier range (I_b) has its chunks there
+// re-streamed by the owner ("halo" units after its own), so the fold needs
+// nothing from another workgroup: after its units the workgroup folds its
+// buffers from the records and raws it wrote itself.  Its waves pull 2-chunk
+// units from an LDS counter; the next unit's chunks and metadata window are
+// in flight while this one computes.
+//
+// Any batch comes out right: the owned ranges of the workgroups cover
+// [0, n) whatever the searches return (I_0 = 0 <= x < n = I_G), a record
+// carries this call's generation only when this call wrote it, and a buffer
+// without its records or with chunks outside the workgroup's streamed range
+// is checksummed serially (unsorted or overlapping batches: correct, slow).
+// Buffers must lie inside the region (the entry point's contract).
+template <int U>
+__device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds) {
+  NVL_TL_DECL();
+  NVL_TL(0);
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
+  const uint64_t B0 = g.nc * blockIdx.x / gridDim.x;
+  const uint64_t B1 = g.nc * (blockIdx.x + 1) / gridDim.x;
+  const uint32_t cnt = (uint32_t)(B1 - B0);
+  const uint32_t nfull = cnt > kTail ? (cnt - kTail) / U : 0u;
+  const uint32_t nunits = nfull + (cnt - nfull * U);
+  uint64_t C0 = B0;       // the halo's first chunk (B0: none) -- known once wave 0 published it
+  uint32_t nhalo = ~0u;   // halo units, ~0u until read
+  auto first_of = [&](uint32_t u) -> uint64_t {
+    if (u >= nunits) return C0 + (uint64_t)(u - nunits) * U;
+    return u < nfull ? B0 + (uint64_t)u * U : B0 + (uint64_t)nfull * U + (u - nfull);
+  };
+  auto count_of = [&](uint32_t u) -> uint32_t {
+    if (u >= nunits) {
+      if (nhalo == ~0u) {  // wave 0 publishes right after the LDS fill: long done by now
+        uint32_t r;
+        while ((r = *region_slot(lds, kSlotReady)) == 0u) __builtin_amdgcn_s_sleep(1);
+        nhalo = uniform_u32(r - 1u);
+        const uint64_t h = *region_slot(lds, kSlotHalo);
+        C0 = B0 - uniform_u64(h);
       }
-      // a chunk-end e: the whole chunk, no unshift (xe = x^0)
-      const uint32_t ze = oe == kChunk ? r1 : q_e.x;
-      const uint32_t re = oe == kChunk ? 0u : quad_prefix(sl, q_e.y, ve, e & 63u);
-      v = gf_mul(xe, acc ^ ze) ^ re;
+      if (u - nunits >= nhalo) return 0u;
+      const uint64_t f = C0 + (uint64_t)(u - nunits) * U;
+      return (uint32_t)min((uint64_t)U, B0 - f);
     }
-    a.out[i] = finish(~v, a.flags);
+    return u < nfull ? (uint32_t)U : 1u;
+  };
+  // Always U chunks' loads (a unit of fewer chunks re-reads its chunk; no
+  // unit reads the grid's first chunk, cache-resident after the first such
+  // load): the compiler counts the loads in flight exactly and waits for
+  // the oldest only -- with loads behind branches it waited for everything
+  // (vmcnt(0)), the next unit's chunks included.
+  auto load_unit = [&](uint64_t ca, uint32_t cu, Chunk (&ch)[U]) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t c = cu ? ca + ((uint32_t)k < cu ? (uint64_t)k : 0u) : 0u;
+      const uintptr_t cs = (uintptr_t)g.grid + c * kChunk;
+      const uint32_t lo = lane_load_off(lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u32x4 v = ld16(cs + 1024u * (uint32_t)j + lo);
+        ch[k].d[4 * j + 0] = v.x; ch[k].d[4 * j + 1] = v.y; ch[k].d[4 * j + 2] = v.z; ch[k].d[4 * j + 3] = v.w;
+      }
+    }
+  };
+
+  // The first two units pre-assigned (wv, wv + 16), so that the memory pipe
+  // stays full across the fill barrier.  Issue order matters: vmcnt retires
+  // in order, so what the waves wait for before the barrier -- the table
+  // blob and the search's first probe -- goes out ahead of the chunks (a
+  // search behind them waited for the whole first wave of chunk loads).
+  uint32_t u = wv;
+  uint64_t ca = first_of(u);
+  uint32_t cu = u < nunits ? count_of(u) : 0u;
+  const bool pre2 = wv + kWavesPerWG < nunits;
+  uint32_t un = pre2 ? wv + kWavesPerWG : 0u;
+  uint32_t cun = pre2 ? count_of(un) : 0u;
+  uint64_t can = pre2 ? first_of(un) : 0u;
+  Chunk cur[U], nxt[U];
+  const RegionFill fill = fill_region_load(ka.tables);
+  const SearchProbe probe = region_probe(g, ca * kChunk, lane);
+  asm volatile("" ::: "memory");
+  load_unit(ca, cu, cur);
+  load_unit(can, cun, nxt);
+  uint64_t cursor = cu ? region_search(g, ca * kChunk, lane, probe) : g.n;
+  NVL_TL(6);
+  WinRaw wr = load_win(g, cursor, lane);
+  fill_region_store(lds, fill, min(nunits, 2u * kWavesPerWG));
+  __syncthreads();
+  NVL_TL(1);
+  // wave 0, after the barrier (searches before it held every wave there):
+  // the owned buffers [I_b, I_b+1) -- I_b is its own first cursor -- and the
+  // halo (the chunks of I_b before B0), published for the halo units and
+  // the fold; its first units' loads are in flight meanwhile
+  if (wv == 0) {
+    const uint64_t Ib = blockIdx.x == 0 ? 0u : (cu ? cursor : region_search(g, B0 * kChunk, lane));
+    const uint64_t Ib1 = blockIdx.x + 1u == gridDim.x ? g.n : region_search(g, B1 * kChunk, lane);
+    const uint64_t sb = Ib < g.n ? g.rel0 + ldg64(g.offsets, Ib) : 0u;
+    const uint64_t hc = (Ib < Ib1 && sb < B0 * kChunk) ? B0 - (sb >> 12) : 0u;  // halo chunks
+    if (lane == 0) {
+      *region_slot(lds, kSlotOwnLo) = (uint32_t)Ib;
+      *region_slot(lds, kSlotOwnHi) = (uint32_t)(Ib >> 32);
+      *region_slot(lds, kSlotEndLo) = (uint32_t)Ib1;
+      *region_slot(lds, kSlotEndHi) = (uint32_t)(Ib1 >> 32);
+      *region_slot(lds, kSlotHalo) = (uint32_t)hc;
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      *region_slot(lds, kSlotReady) = (uint32_t)((hc + U - 1u) / U) + 1u;
+    }
   }
+  const LaneBase lb = make_lane_base(lane);
+  if (!cu) {  // no pre-assigned unit (a range of fewer than 16 units): pull one, maybe a halo unit
+    u = pull_unit(lds, lane, kRCtrOff);
+    cu = count_of(u);
+    ca = first_of(u);
+    load_unit(ca, cu, cur);
+    cursor = cu && u < nunits ? region_search(g, ca * kChunk, lane) : g.n;
+    wr = load_win(g, cursor, lane);
+  }
+  if (cu && !pre2) {  // no pre-assigned second unit
+    un = pull_unit(lds, lane, kRCtrOff);
+    cun = count_of(un);  // (first: a halo unit's reads the halo)
+    can = first_of(un);
+    load_unit(can, cun, nxt);
+  }
+
+  // One unit: its window (loaded a unit ago) gives the next unit's cursor
+  // and window load, it computes from `buf` (its chunks, loaded a unit ago),
+  // and the unit after next is pulled and its chunks go out into `buf` --
+  // one fixed count of loads per unit.  The buffers alternate (ping-pong):
+  // a copy nxt -> cur made the compiler wait for the loads just issued.
+  auto step = [&](Chunk (&buf)[U]) {
+    const bool halo = u >= nunits;
+    const Win w = make_win(g, wr, cursor, lane);
+    uint64_t ncur = g.n;
+    if (cun && un < nunits) {  // the next unit's cursor: the first buffer of this window ending after its start
+      const uint64_t m = __ballot(w.valid && w.e > can * kChunk);
+      ncur = m ? cursor + (uint64_t)__builtin_ctzll(m) : min(cursor + 64u, g.n);
+    }
+    const WinRaw nwr = load_win(g, ncur, lane);
+
+    const LaneEv le = lane_events(w, ca * kChunk, (ca + cu) * kChunk);
+    const bool any_ev = !halo && __ballot(le.sv || le.ev) != 0u;
+    uint32_t Lf[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) Lf[k] = 0u;
+    if (any_ev) first_lanes<U>(le, Lf);
+    uint32_t raw[U], pre[U], cp[U][3];
+    if (cu == (uint32_t)U) {
+      uint32_t wd[U][16];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) wd[k][q] = buf[k].d[q];
+        row_transpose(wd[k]);
+      }
+      chains_scan<U>(lds, lb, wd, lane, raw, pre, cp);
+    } else {  // the range's single-chunk units
+      uint32_t wd[1][16], r1[1], p1[1], c1[1][3];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wd[0][q] = buf[0].d[q];
+      row_transpose(wd[0]);
+      chains_scan<1>(lds, lb, wd, lane, r1, p1, c1);
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        raw[k] = r1[0];
+        pre[k] = p1[0];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) cp[k][m] = c1[0][m];
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if ((uint32_t)k < cu) g.raws[ca + k] = raw[k];
+    }
+    if (halo) {
+      if (ca == C0) {  // the halo's first chunk holds I_b's start: its one record
+        const uint64_t ib = ((uint64_t)*region_slot(lds, kSlotOwnHi) << 32) | *region_slot(lds, kSlotOwnLo);
+        const uint64_t s = g.rel0 + ldg64(g.offsets, uniform_u64(ib));
+        const uint32_t os = uniform_u32((uint32_t)(s & (kChunk - 1u)));
+        if (os) {
+          const uint32_t L = os >> 6, c = (os >> 4) & 3u;
+          const uint32_t x = c == 1u ? cp[0][0] : (c == 2u ? cp[0][1] : cp[0][2]);
+          const uint4 r = make_uint4(lane_u32(pre[0], L), c ? lane_u32(x, L) : 0u, g.gen, 0u);
+          if (lane == 0) g.qs[ib] = r;
+        }
+      }
+    } else if (any_ev || (cursor + 64u < g.n && lane_u64(w.s, 63) < (ca + cu) * kChunk)) {
+      // (a unit with no event and no buffer running past its window -- most
+      // of config 3's -- has nothing to record)
+      region_events<U>(g, w, cursor, ca, cu, pre, Lf, cp, le, lane);
+    }
+
+    u = un;
+    ca = can;
+    cu = cun;
+    cursor = ncur;
+    wr = nwr;
+    cun = 0u;
+    if (cu) {
+      un = pull_unit(lds, lane, kRCtrOff);
+      cun = count_of(un);
+      can = first_of(un);
+    }
+    load_unit(can, cun, buf);
+  };
+  // (the first step peeled: the loop is entered from its straight-line end
+  // only, so the prologue's optional loads do not blur the in-flight count)
+  if (cu) {
+    step(cur);
+    while (cu) {
+      step(nxt);
+      if (!cu) break;
+      step(cur);
+    }
+  }
+
+  // The fold of the owned buffers, one thread each, from this workgroup's
+  // own records and raws (visible after the barrier), in 64-buffer slices
+  // claimed from an LDS counter: a wave claims its first slice as it runs
+  // out of units and has that slice's batch-only inputs in flight across the
+  // barrier, so the last waves to finish find the slices taken.
+  NVL_TL(2);
+  uint32_t r;
+  while ((r = *region_slot(lds, kSlotReady)) == 0u) __builtin_amdgcn_s_sleep(1);  // (wave 0 has published)
+  const uint64_t ib = ((uint64_t)*region_slot(lds, kSlotOwnHi) << 32) | *region_slot(lds, kSlotOwnLo);
+  const uint64_t ib1 = ((uint64_t)*region_slot(lds, kSlotEndHi) << 32) | *region_slot(lds, kSlotEndLo);
+  const uint64_t c0w = B0 - *region_slot(lds, kSlotHalo);  // the first chunk streamed here
+  const uint64_t nsl = ib1 > ib ? (ib1 - ib + 63u) / 64u : 0u;
+  auto claim = [&]() -> uint64_t {
+    uint32_t v = 0;
+    if (lane == 0)
+      v = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)region_slot(lds, kSlotTail), 1u,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return uniform_u32(v);
+  };
+  uint64_t k = claim();
+  FoldIn f;
+  if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
+  __syncthreads();
+  NVL_TL(3);
+  const uint8_t* lsl = lds + (kRSliceOff - kSliceOff);
+  while (k < nsl) {
+    const uint64_t i = ib + 64u * k + (uint64_t)lane;
+    if (i < ib1) {
+      const uint4 q_s = g.qs[i], q_e = g.qe[i];  // (not written for a buffer without that event: unused then)
+      NVL_TL_WAIT(4, q_s.x);
+      uint32_t v = 0u;
+      if (!(f.fast && fold_out(g, lds, lsl, lb, lane, f, q_s, q_e, v)))
+        v = serial_raw(ka.tables + kGSlice, f.ninit, g.grid + f.s, f.L);  // (outside the region too: the caller's memory)
+      NVL_TL_WAIT(5, v);
+      ka.out[i] = finish(~v, ka.flags);
+    }
+    k = claim();
+    if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
+  }
+  NVL_TL_END();
+}
+
+__global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRLdsBytes];
+  run_region<NVL_FAST_U>(g, ka, lds);
 }
 
 // Synthetic stream: one thread per 8-byte word.
@@ -3542,44 +3781,34 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
 // by region_len / 4096 + 2 whatever the region's alignment).
 static inline size_t align256(size_t v) { return (v + 255u) / 256u * 256u; }
 size_t region_ws_bytes(uint64_t region_len, uint64_t n) {
-  return align256((region_len / dev::kChunk + 2u) * 4u) + 2u * align256(n * 8u);
+  return align256((region_len / dev::kChunk + 2u) * 4u) + 2u * align256(n * 16u);
 }
 
 hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* ws) {
   if (n == 0) return hipSuccess;
-  if (!lc.counter) return hipErrorInvalidValue;
   const uintptr_t O = (uintptr_t)region & ~(uintptr_t)(dev::kChunk - 1u);
   const uint64_t rel0 = (uintptr_t)region - O;
   const uint64_t nc = (rel0 + region_len + dev::kChunk - 1u) / dev::kChunk;
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* raws = reinterpret_cast<uint32_t*>(w);
-  uint2* qs = reinterpret_cast<uint2*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
-  uint2* qe = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 8u));
-  // A process-wide call generation (never 0, the zeroed block's value): the
-  // fold kernel trusts the flag word only when it carries this call's.
+  uint4* qs = reinterpret_cast<uint4*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
+  uint4* qe = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 16u));
+  // A process-wide call generation (never 0, the zeroed workspace's value):
+  // the fold trusts an event record only when it carries this call's.
   static std::atomic<uint32_t> s_gen{0};
   uint32_t gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
   if (gen == 0u) gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
-  dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, raws, qs, qe,
-                    lc.counter, gen};
+  dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, init, init_all,
+                    raws, qs, qe, gen};
   dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, nullptr};
-  const uint32_t grid = grid_for(lc.num_cu, nc);  // >= 1: the waves also check the batch
-  if (lc.ev_start)
+  const uint32_t grid = grid_for(lc.num_cu, nc);  // >= 1 (nc >= 1: n > 0 buffers inside the region)
+  if (lc.ev_start || lc.ev_stop)
     hipExtLaunchKernelGGL(dev::crc32c_region_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, lc.ev_start,
-                          nullptr, 0u, g, ka);
+                          lc.ev_stop, 0u, g, ka);
   else
     hipLaunchKernelGGL(dev::crc32c_region_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  dev::RegionFold f{reinterpret_cast<const uint8_t*>(O), rel0, offsets, lengths, n, init, init_all, flags, raws, qs,
-                    qe, lc.tables, out, lc.counter, gen};
-  const dim3 fg((uint32_t)((n + 255u) / 256u));
-  if (lc.ev_stop)
-    hipExtLaunchKernelGGL(dev::crc32c_region_fold_kernel, fg, dim3(256), 0, lc.stream, nullptr, lc.ev_stop, 0u, f);
-  else
-    hipLaunchKernelGGL(dev::crc32c_region_fold_kernel, fg, dim3(256), 0, lc.stream, f);
   return hipGetLastError();
 }
 

@@ -498,6 +498,30 @@ def region_fold(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     return (~v) & 0xFFFFFFFF
 
 
+def region_fold_direct(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
+    """The region kernel's fold as it computes a buffer spanning at most two
+    chunks: every term moved straight to e by one multiply (three independent
+    multiplies instead of a chain).  Longer buffers: region_fold."""
+    if L < REGION_DIRECT:
+        return (~raw_bytes((~init) & 0xFFFFFFFF, mem[s:s + L])) & 0xFFFFFFFF
+    e = s + L
+    c0, os_ = s >> 12, s & 4095
+    c1, oe = (e - 1) >> 12, e - ((e - 1) >> 12 << 12)
+    if c1 > c0 + 1:
+        return region_fold(mem, raws, qe, s, L, init)
+    ninit = (~init) & 0xFFFFFFFF
+    qs = qe[("s", c0, os_)] if os_ else 0
+    T = (piece_prefix_raw(mem, s) if os_ else 0) ^ ninit
+    ze = raws[c1] if oe == 4096 else qe[("e", c1, oe)]
+    re = 0 if oe == 4096 else piece_prefix_raw(mem, e)
+    back = lambda v: unshift(v, 4096 - oe)  # x^(-8(4096 - oe))
+    if c1 == c0 + 1:
+        v = shift(qs ^ raws[c0], oe) ^ shift(T, L) ^ back(ze) ^ re
+    else:
+        v = back(ze ^ qs) ^ shift(T, L) ^ re
+    return (~v) & 0xFFFFFFFF
+
+
 def _xinv(v: int) -> int:
     """v * x^-1 mod P (reflected): the inverse of one zero-bit feed."""
     return (((v ^ POLY) << 1) | 1) & 0xFFFFFFFF if v & ONE else (v << 1) & 0xFFFFFFFF
@@ -524,7 +548,7 @@ def region_batch(mem: bytes, bufs, inits):
     for s, L in bufs:
         for kind, c, o in region_events(s, s + L, L):
             qe[(kind, c, o)] = pres[c][o >> 6]
-    return [region_fold(mem, raws, qe, s, L, i) for (s, L), i in zip(bufs, inits)]
+    return [region_fold_direct(mem, raws, qe, s, L, i) for (s, L), i in zip(bufs, inits)]
 
 
 def chain_checkpoints(piece: bytes):

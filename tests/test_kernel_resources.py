@@ -41,7 +41,7 @@ def usage(tmp_path_factory):
 
 
 HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_var_kernel", "crc32c_var_fused_kernel",
-       "crc32c_region_kernel", "crc32c_region_fold_kernel", "crc32c_chunks_kernel",
+       "crc32c_region_kernel", "crc32c_chunks_kernel",
        "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel"]
 # SGPR spills go to VGPR lanes (v_writelane/v_readlane), not memory: a bound
 # per kernel so that a jump shows.  The fused kernel parks plan-phase scalars

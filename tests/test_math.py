@@ -199,9 +199,10 @@ def test_region_path_model(port, seed):
         bufs.append((p, L))
         inits.append(rng.getrandbits(32) if rng.random() < 0.5 else 0)
         p += L + rng.choice([0, 0, 4, 5, 1, 64 - (p + L) % 64])
-    # starts/ends exactly on piece and chunk boundaries
-    bufs += [(4096, 64), (4096 * 2 - 64, 64 + 4096)]
-    inits += [0, 7]
+    # starts/ends exactly on piece and chunk boundaries; two whole chunks
+    # (L = 8192: the longest buffer the direct fold takes); three chunks
+    bufs += [(4096, 64), (4096 * 2 - 64, 64 + 4096), (4096, 8192), (100, 8192), (4095, 4098)]
+    inits += [0, 7, 3, 0, 9]
     got = km.region_batch(mem, bufs, inits)
     want = [port.extend(i, mem[s:s + L]) for (s, L), i in zip(bufs, inits)]
     assert got == want

@@ -48,6 +48,11 @@ __device__ unsigned long long g_tl[8 * 65536];
 }  // namespace nvl
 #define NVL_TL_DECL() unsigned long long tl_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define NVL_TL(k) (tl_[(k)] = __builtin_amdgcn_s_memrealtime())
+#define NVL_TL_WAIT(k, v)                        \
+  do {                                           \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(v)); \
+    NVL_TL(k);                                   \
+  } while (0)
 #define NVL_TL_END()                                                                        \
   do {                                                                                      \
     const uint32_t wave_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);              \

@@ -3111,7 +3111,7 @@ __device__ __forceinline__ uint32_t fold_sh4096(const uint32_t* sh, uint32_t acc
 // caller then checksums the buffer serially.
 struct FoldIn {
   uint64_t s, L;
-  uint32_t ninit, xs, xe, xo, xl;  // x^(8(4096 - os)), x^(-8(4096 - oe)), x^(8 oe), x^(8L) (L < 8192)
+  uint32_t ninit, xs, xe, xt;  // x^(8(4096 - os)), x^(-8(4096 - oe)), x^(8L) (one chunk) / x^(8(8192 - os)) (two)
   u32x4 vs, ve;
   bool fast;  // inside the region, >= kRegionDirect bytes, every chunk streamed by this workgroup
 };
@@ -3131,8 +3131,8 @@ __device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* t
   f.ve = ld16c((uintptr_t)g.grid + (oe == kChunk ? e - 16u : (e & ~(uint64_t)15)));
   f.xs = tables[kTabXp8 + kChunk - os];
   f.xe = tables[kTabXm8 + (kChunk - oe)];
-  f.xo = tables[kTabXp8 + oe];
-  f.xl = tables[kTabXp8 + min(e - s, (uint64_t)kXp8Len - 1u)];
+  const uint64_t c0 = s >> 12;
+  f.xt = tables[kTabXp8 + (c1 == c0 ? e - s : (c1 == c0 + 1u ? 2u * kChunk - os : 0u))];
   return f;
 }
 
@@ -3213,13 +3213,16 @@ __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds
   const uint32_t T = (os ? quad_prefix_lds(lsl, lb, q_s.y, f.vs, s & 63u) : 0u) ^ f.ninit;  // R(s) ^ ~init, at s
   const uint32_t ze = oe == kChunk ? r1 : q_e.x;                         // chunk c1's bytes before e, at its end
   const uint32_t re = oe == kChunk ? 0u : quad_prefix_lds(lsl, lb, q_e.y, f.ve, e & 63u);  // R(e), at e
-  if (c1 <= c0 + 1u) {
-    // Everything moved straight to e, three independent multiplies:
-    //   c1 = c0 + 1: (Qe(s) ^ raw c0) x^(8 oe) ^ T x^(8L) ^ Ze x^(-8(4096 - oe)) ^ R(e)
-    //   c1 = c0:     (Ze ^ Qe(s)) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e)
-    const bool two = c1 != c0;
-    v = gf_mul_lds(lsl, lb, f.xo, two ? qs ^ r0 : 0u) ^ gf_mul_lds(lsl, lb, f.xl, T) ^
-        gf_mul_lds(lsl, lb, f.xe, two ? ze : ze ^ qs) ^ re;
+  if (c1 == c0) {  // one chunk: (Ze ^ Qe(s)) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e), two independent multiplies
+    v = gf_mul_lds(lsl, lb, f.xe, ze ^ qs) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ re;
+    return true;
+  }
+  if (c1 == c0 + 1u) {
+    // two chunks, everything at chunk c1's end, then one unshift:
+    //   (shift4096(Qe(s) ^ raw c0) ^ T x^(8(8192 - os)) ^ Ze) x^(-8(4096 - oe)) ^ R(e)
+    // (two multiplies and two column shifts: the fold is VALU-bound, and a
+    // third multiply in parallel cost more than the longer chain)
+    v = gf_mul_lds(lsl, lb, f.xe, sh4096_lds(lds, qs ^ r0, lane) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ ze) ^ re;
     return true;
   }
   // Longer: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) at chunk c0's end, the chunks in between, unshifted from c1's end
@@ -3318,34 +3321,31 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     }
   };
 
-  // The first two units pre-assigned (wv, wv + 16), so that the memory pipe
-  // stays full across the fill barrier.  Issue order matters: vmcnt retires
-  // in order, so what the waves wait for before the barrier -- the table
-  // blob and the search's first probe -- goes out ahead of the chunks (a
-  // search behind them waited for the whole first wave of chunk loads).
+  // First unit pre-assigned.  Issue order matters: vmcnt retires in order,
+  // so what the waves wait for before the fill barrier -- the table blob
+  // and the search's first probe -- goes out ahead of the unit's chunks.
+  // (Two pre-assigned units per wave, 64 MB in flight at the start, delayed
+  // the probes' return to ~10 us and lost ~8 us: rejected.)
   uint32_t u = wv;
   uint64_t ca = first_of(u);
   uint32_t cu = u < nunits ? count_of(u) : 0u;
-  const bool pre2 = wv + kWavesPerWG < nunits;
-  uint32_t un = pre2 ? wv + kWavesPerWG : 0u;
-  uint32_t cun = pre2 ? count_of(un) : 0u;
-  uint64_t can = pre2 ? first_of(un) : 0u;
+  uint32_t un = 0u, cun = 0u;
+  uint64_t can = 0u;
   Chunk cur[U], nxt[U];
   const RegionFill fill = fill_region_load(ka.tables);
   const SearchProbe probe = region_probe(g, ca * kChunk, lane);
   asm volatile("" ::: "memory");
   load_unit(ca, cu, cur);
-  load_unit(can, cun, nxt);
   uint64_t cursor = cu ? region_search(g, ca * kChunk, lane, probe) : g.n;
   NVL_TL(6);
   WinRaw wr = load_win(g, cursor, lane);
-  fill_region_store(lds, fill, min(nunits, 2u * kWavesPerWG));
+  fill_region_store(lds, fill, min(nunits, (uint32_t)kWavesPerWG));
   __syncthreads();
   NVL_TL(1);
   // wave 0, after the barrier (searches before it held every wave there):
   // the owned buffers [I_b, I_b+1) -- I_b is its own first cursor -- and the
   // halo (the chunks of I_b before B0), published for the halo units and
-  // the fold; its first units' loads are in flight meanwhile
+  // the fold; its first unit's loads are in flight meanwhile
   if (wv == 0) {
     const uint64_t Ib = blockIdx.x == 0 ? 0u : (cu ? cursor : region_search(g, B0 * kChunk, lane));
     const uint64_t Ib1 = blockIdx.x + 1u == gridDim.x ? g.n : region_search(g, B1 * kChunk, lane);
@@ -3370,19 +3370,17 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     cursor = cu && u < nunits ? region_search(g, ca * kChunk, lane) : g.n;
     wr = load_win(g, cursor, lane);
   }
-  if (cu && !pre2) {  // no pre-assigned second unit
+
+  // Per unit: the next unit is pulled and its chunks go out (in flight
+  // while this one computes), this unit's window (loaded a unit ago) gives
+  // the next unit's cursor and window load, this unit computes -- one fixed
+  // count of loads per unit.  (Loads at the end of the unit, ping-pong
+  // buffers: 8 % slower on v, rejected.)
+  while (cu) {
     un = pull_unit(lds, lane, kRCtrOff);
     cun = count_of(un);  // (first: a halo unit's reads the halo)
     can = first_of(un);
     load_unit(can, cun, nxt);
-  }
-
-  // One unit: its window (loaded a unit ago) gives the next unit's cursor
-  // and window load, it computes from `buf` (its chunks, loaded a unit ago),
-  // and the unit after next is pulled and its chunks go out into `buf` --
-  // one fixed count of loads per unit.  The buffers alternate (ping-pong):
-  // a copy nxt -> cur made the compiler wait for the loads just issued.
-  auto step = [&](Chunk (&buf)[U]) {
     const bool halo = u >= nunits;
     const Win w = make_win(g, wr, cursor, lane);
     uint64_t ncur = g.n;
@@ -3404,14 +3402,14 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
 #pragma unroll
       for (int k = 0; k < U; ++k) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) wd[k][q] = buf[k].d[q];
+        for (int q = 0; q < 16; ++q) wd[k][q] = cur[k].d[q];
         row_transpose(wd[k]);
       }
       chains_scan<U>(lds, lb, wd, lane, raw, pre, cp);
     } else {  // the range's single-chunk units
       uint32_t wd[1][16], r1[1], p1[1], c1[1][3];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) wd[0][q] = buf[0].d[q];
+      for (int q = 0; q < 16; ++q) wd[0][q] = cur[0].d[q];
       row_transpose(wd[0]);
       chains_scan<1>(lds, lb, wd, lane, r1, p1, c1);
 #pragma unroll
@@ -3450,23 +3448,8 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     cu = cun;
     cursor = ncur;
     wr = nwr;
-    cun = 0u;
-    if (cu) {
-      un = pull_unit(lds, lane, kRCtrOff);
-      cun = count_of(un);
-      can = first_of(un);
-    }
-    load_unit(can, cun, buf);
-  };
-  // (the first step peeled: the loop is entered from its straight-line end
-  // only, so the prologue's optional loads do not blur the in-flight count)
-  if (cu) {
-    step(cur);
-    while (cu) {
-      step(nxt);
-      if (!cu) break;
-      step(cur);
-    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) cur[k] = nxt[k];
   }
 
   // The fold of the owned buffers, one thread each, from this workgroup's

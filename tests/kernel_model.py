@@ -500,8 +500,9 @@ def region_fold(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
 
 def region_fold_direct(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     """The region kernel's fold as it computes a buffer spanning at most two
-    chunks: every term moved straight to e by one multiply (three independent
-    multiplies instead of a chain).  Longer buffers: region_fold."""
+    chunks (one chunk: every term moved straight to e, two independent
+    multiplies; two chunks: every term at chunk c1's end, one unshift).
+    Longer buffers: region_fold."""
     if L < REGION_DIRECT:
         return (~raw_bytes((~init) & 0xFFFFFFFF, mem[s:s + L])) & 0xFFFFFFFF
     e = s + L
@@ -516,7 +517,7 @@ def region_fold_direct(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     re = 0 if oe == 4096 else piece_prefix_raw(mem, e)
     back = lambda v: unshift(v, 4096 - oe)  # x^(-8(4096 - oe))
     if c1 == c0 + 1:
-        v = shift(qs ^ raws[c0], oe) ^ shift(T, L) ^ back(ze) ^ re
+        v = back(apply_op(SH4096, qs ^ raws[c0]) ^ shift(T, 8192 - os_) ^ ze) ^ re
     else:
         v = back(ze ^ qs) ^ shift(T, L) ^ re
     return (~v) & 0xFFFFFFFF

@@ -3243,10 +3243,9 @@ __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds
 
 // LDS slots in the region image's lane-63 column (never read by the lane
 // shifts): row r at r * 256 + 252.  Row 16 (T[1][0][63]) is 0 in the blob.
-// (an LDS-qualified pointer: through a generic one the volatile accesses
-// became flat loads, which count in vmcnt -- every wait on them was a
-// vmcnt(0) that also waited for the next unit's chunks)
-typedef volatile __attribute__((address_space(3))) uint32_t lds_vu32;
+// (generic pointer: the volatile accesses become flat loads, which count in
+// vmcnt as well; an LDS-qualified pointer was measured slower, see load_unit)
+typedef volatile uint32_t lds_vu32;
 __device__ __forceinline__ lds_vu32* region_slot(uint8_t* lds, uint32_t r) {
   return (lds_vu32*)(lds + kRNibOff + r * 256u + 252u);
 }
@@ -3302,15 +3301,15 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
     }
     return u < nfull ? (uint32_t)U : 1u;
   };
-  // Always U chunks' loads (a unit of fewer chunks re-reads its chunk; no
-  // unit reads the grid's first chunk, cache-resident after the first such
-  // load): the compiler counts the loads in flight exactly and waits for
-  // the oldest only -- with loads behind branches it waited for everything
-  // (vmcnt(0)), the next unit's chunks included.
+  // (Loads behind the branch: the compiler then waits vmcnt(0) at the top
+  // of the unit, the next unit's chunks included.  Unconditional loads with
+  // exact wait counts were measured 1.5-2 us slower on v / r -- waves that
+  // run further ahead only queue more requests -- and were rejected.)
   auto load_unit = [&](uint64_t ca, uint32_t cu, Chunk (&ch)[U]) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const uint64_t c = cu ? ca + ((uint32_t)k < cu ? (uint64_t)k : 0u) : 0u;
+      if ((uint32_t)k >= cu) continue;
+      const uint64_t c = ca + (uint64_t)k;
       const uintptr_t cs = (uintptr_t)g.grid + c * kChunk;
       const uint32_t lo = lane_load_off(lane);
 #pragma unroll
@@ -3467,7 +3466,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   auto claim = [&]() -> uint64_t {
     uint32_t v = 0;
     if (lane == 0)
-      v = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t*)region_slot(lds, kSlotTail), 1u,
+      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail)), 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return uniform_u32(v);
   };

@@ -12,7 +12,7 @@ around each call, median of R reps), every result checked.
   r        10^5 buffers of 3364..4109 B (the n+1 of data blocks at block_size 4096)
            at stride length+4, nvl_crc32c_batch_dev
 v, g and r are checked CRC by CRC against the oracle."""
-import argparse, ctypes, json, os, sys
+import argparse, time, ctypes, json, os, sys
 import numpy as np, torch
 ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
@@ -20,6 +20,7 @@ from nvlevelz_amd import _lib
 import oracle
 ap = argparse.ArgumentParser(); ap.add_argument("--lib"); ap.add_argument("--configs", default="2,3,4")
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--warm-ms", type=float, default=60.0)
 a = ap.parse_args()
 lib = _lib.lib
 if a.lib:
@@ -35,13 +36,30 @@ g = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
 p = oracle.port()
 
 
+SUSTAINED = {}
+
+
 def timeit(fn, reps):
-    for _ in range(3): fn()
-    torch.cuda.synchronize()
+    """Median of single calls (events around each), after a warm-up of
+    a.warm_ms of back-to-back calls (the GPU's sustained-load state: the
+    first ~30 ms of load run ~15 % slower, profiles/r04_clocks_cfg2.jsonl);
+    also the sustained period of reps back-to-back calls (SUSTAINED)."""
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(10): fn()
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 > a.warm_ms * 1e-3:
+            break
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
     for j in range(reps):
         ev[2*j].record(); fn(); ev[2*j+1].record()
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps): fn()
+    e1.record()
+    torch.cuda.synchronize()
+    SUSTAINED["period"] = e0.elapsed_time(e1) * 1e-3 / reps
     return float(np.median([ev[2*j].elapsed_time(ev[2*j+1]) for j in range(reps)])) * 1e-3
 
 
@@ -128,8 +146,10 @@ for c in a.configs.split(","):
         raise SystemExit(f"unknown config {c}")
     t = timeit(fn, a.reps if c != "4" else max(3, a.reps // 4))
     res = out.cpu().numpy().view(np.uint32)
+    ps = SUSTAINED["period"]
     print(json.dumps({"config": c, "n": int(n), "bytes": int(alg), "median_us": round(t * 1e6, 1),
                       "GB/s": round(alg / t / 1e9, 1), "GiB/s": round(alg / t / 2**30, 1),
-                      "frac_of_8TBs": round(alg / t / 8e12, 4), "ok": bool(check(res))}), flush=True)
+                      "frac_of_8TBs": round(alg / t / 8e12, 4), "sustained_period_us": round(ps * 1e6, 1),
+                      "sustained_frac": round(alg / ps / 8e12, 4), "ok": bool(check(res))}), flush=True)
     del buf, keep
     torch.cuda.empty_cache()

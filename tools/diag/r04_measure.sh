@@ -11,7 +11,7 @@ STEPS=${*:-configs prof shims iso pmc}
 for s in $STEPS; do
   case $s in
     configs)
-      timeout -k 10 400 python3 $R/tools/bench_configs.py --configs 2,3R,vR,rR,4,3,v,r --reps 30 \
+      timeout -k 10 400 python3 $R/tools/bench_configs.py --configs 2,3R,vR,rR,4,big1,3,v,r --reps 30 \
         > $O/r04_configs.jsonl 2> $O/r04_configs.err || exit 1 ;;
     prof)
       (cd /tmp && TMPDIR=/tmp bash $R/tools/diag/prof_region.sh r04 cfg3 var4097 rand > $O/r04_prof_region.log 2>&1) || exit 1 ;;

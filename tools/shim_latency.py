@@ -61,7 +61,8 @@ def table_handles(img_len, nblocks):
 
 import torch
 torch.cuda.set_device(0)
-assert L.nvl_crc32c_init(0) == 0
+rc0 = L.nvl_crc32c_init(0)
+assert rc0 == 0, f"nvl_crc32c_init: {rc0}"
 sptr = torch.cuda.current_stream().cuda_stream
 for mib in [float(x) for x in a.sizes.split(",")]:
     nblocks = max(1, int(mib * 2**20 / 4101))

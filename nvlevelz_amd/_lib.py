@@ -103,6 +103,14 @@ def load() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C nvlevelz_amd/csrc` (the batch CRC32C path has no fallback)")
+    # One HIP runtime per process.  PyTorch ships its own libamdhip64; loaded
+    # after ours (/opt/rocm's, by path) it becomes a second runtime and the
+    # first HIP call here found no device (ENODEV, tools/shim_latency.py).
+    # Importing torch first makes our library bind to the copy already loaded.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # noqa: BLE001 -- a C-ABI-only user without torch: /opt/rocm's runtime
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)

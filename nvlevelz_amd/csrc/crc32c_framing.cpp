@@ -19,7 +19,7 @@
 // flags = 0 crossover (bytes checksummed per host-resident call), from
 // profiles/r04_shim_latency.jsonl.
 #ifndef NVL_FRAMING_DEFAULT_GPU_MIN_BYTES
-#define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES (8ull << 20)
+#define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES (16ull << 20)  // host wins below ~17 MiB, GPU from 32 MiB
 #endif
 
 namespace nvl {

@@ -60,7 +60,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=1000)  # ~67 ms: past the ~30 ms ramp of a sustained load (profiles/r04_clocks_cfg2.jsonl)
     ap.add_argument("--config", choices=["cfg2", "cfg5"], default="cfg2")
     ap.add_argument("--blocks", type=int, default=None, help="override blocks per GPU (cfg2)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0,

@@ -2163,6 +2163,57 @@ __global__ __launch_bounds__(256) void crc32c_fold_kernel(const uint32_t* __rest
   }
 }
 
+// Two-level fold for buffers of more than kChunkParallelMaxJ chunks (a lone
+// 1 GiB buffer: J = 262144): level 1 folds segments of S chunk raws (one
+// wave each, the whole grid busy), level 2 folds each buffer's G segment
+// raws -- the same fold with the step "S chunks".  Row `row` holds J
+// elements, element e sits at its end, consecutive elements `step` apart
+// (x^(8 * bytes)); segment g = elements [J - (G - g) S, J - (G - g - 1) S)
+// (the first one clipped at 0).  A wave's lane l folds the run of R =
+// ceil(S / 64) elements ending R (63 - l) before the segment end through the
+// byte-sliced step table (built in LDS), multiplies by m[l] = step^(R (63 -
+// l)) (host-computed), and the lanes XOR-reduce: G > 1 writes the segment's
+// raw to dst[row * G + g], G == 1 writes finish(~raw) to dst[row].
+struct FoldSeg {
+  const uint32_t* src;
+  uint64_t rows;
+  uint32_t J, S, G, step;
+  uint32_t m[64];
+  uint32_t* dst;
+  uint32_t flags;
+};
+__global__ __launch_bounds__(256) void crc32c_fold_seg_kernel(FoldSeg a) {
+  __shared__ uint32_t sh[1024];  // sh[j][b] = (b << 8j) * step
+  for (uint32_t t = threadIdx.x; t < 1024u; t += blockDim.x) sh[t] = nvl::gf_mul(a.step, (t & 255u) << (8u * (t >> 8)));
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t R = (a.S + 63u) / 64u;
+  const uint32_t m = a.m[lane];
+  const uint64_t items = a.rows * a.G;
+  const uint64_t wpb = blockDim.x >> 6;
+  const uint64_t nw = (uint64_t)gridDim.x * wpb;
+  for (uint64_t it = (uint64_t)blockIdx.x * wpb + uniform_u32(threadIdx.x >> 6); it < items; it += nw) {
+    const uint64_t row = it / a.G;
+    const uint32_t g = (uint32_t)(it - row * a.G);
+    const int64_t seg0 = (int64_t)a.J - (int64_t)(a.G - g) * (int64_t)a.S;  // first element of the segment
+    const int64_t c0 = seg0 + (int64_t)a.S - (int64_t)R * (int64_t)(64u - lane);
+    const uint32_t* rb = a.src + row * a.J;
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < R; ++k) {
+      const int64_t c = c0 + (int64_t)k;
+      const uint32_t r = (c >= 0 && c >= seg0) ? rb[c] : 0u;
+      acc = sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)] ^ r;
+    }
+    acc = nvl::gf_mul(m, acc);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+    if (lane == 0) {
+      if (a.G > 1) a.dst[it] = acc;
+      else a.dst[row] = finish(~acc, a.flags);
+    }
+  }
+}
+
 #ifndef NVL_VAR_BUFS
 #define NVL_VAR_BUFS 1  // 1: scheduler C when every buffer has <= kBufsMaxJ chunks
 #endif
@@ -3597,9 +3648,28 @@ static inline size_t recs_part(int num_cu, uint64_t len, uint64_t n) {
 // 4096, J > 1: aligned when base and stride are), the n*J chunk raws if larger.
 constexpr uint32_t kChunkParallelMaxJ = 1024;  // fold runs of <= 16 raws per lane (config 4: J = 512, R = 8)
 
+constexpr uint32_t kFoldSeg = 1024;  // level-1 segment of the two-level fold (runs of 16 raws per lane)
+
+static inline uint64_t fold_segments(uint32_t J) { return (J + kFoldSeg - 1u) / kFoldSeg; }
+
+// the n*J chunk raws, and for J > kChunkParallelMaxJ the n*G segment raws after them
 static inline size_t chunk_raws_bytes(uint64_t len, uint64_t n) {
-  return (len > dev::kChunk && len % dev::kChunk == 0 && len / dev::kChunk <= kChunkParallelMaxJ)
-             ? n * (len / dev::kChunk) * sizeof(uint32_t) : 0;
+  if (!(len > dev::kChunk && len % dev::kChunk == 0)) return 0;
+  const uint64_t J = len / dev::kChunk;
+  const size_t raws = (n * J * sizeof(uint32_t) + 255u) / 256u * 256u;
+  return J <= kChunkParallelMaxJ ? n * J * sizeof(uint32_t) : raws + n * fold_segments((uint32_t)J) * sizeof(uint32_t);
+}
+
+// x^(8 bytes) and the lane multipliers step^(R (63 - l)) of a fold whose
+// lanes take runs of R elements (host GF(2) arithmetic, crc32c_math.h).
+static void fold_powers(uint64_t step_bytes, uint32_t S, uint32_t* step, uint32_t m[64]) {
+  PowTable pw;
+  build_pow_table(&pw);
+  *step = xpow8(pw.x2n, step_bytes);
+  const uint32_t R = (S + 63u) / 64u;
+  const uint32_t sR = xpow8(pw.x2n, step_bytes * R);
+  m[63] = kOne;
+  for (int l = 62; l >= 0; --l) m[l] = gf_mul(m[l + 1], sR);
 }
 size_t fixed_recs_bytes(int num_cu, uint64_t len, uint64_t n) {
   const size_t cr = chunk_raws_bytes(len, n);
@@ -3635,11 +3705,44 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
     if (eh != hipSuccess || !body) return eh;
     ev_start = nullptr;
   }
-  // Chunk-parallel (every chunk a scheduler-A pass, then the per-buffer fold)
-  // while a fold lane's serial run R = ceil(J/64) stays short: the fold is one
-  // wave per buffer, so a few huge buffers (n = 1 x 1 GiB: R = 4096) would
-  // fold for longer than they stream; those take scheduler B, whose units
-  // split the chunk space over the whole grid (bench_configs `big1`).
+  // Chunk-parallel: every chunk a scheduler-A pass, then the per-buffer
+  // fold -- one wave per buffer while a lane's serial run R = ceil(J/64)
+  // stays short (J <= 1024), else two levels (crc32c_fold_seg_kernel:
+  // segments of 1024 chunks over the whole grid, then the segments per
+  // buffer), so a lone 1 GiB buffer (bench_configs `big1`) streams at
+  // scheduler A's rate too.
+  if (aligned && J > kChunkParallelMaxJ) {
+    const uint64_t T = n * (uint64_t)J;
+    const uint32_t jsh = (J & (J - 1u)) == 0u ? (uint32_t)__builtin_ctz(J) : 64u;
+    dev::ChunkGeom cg{base, stride, T, J, jsh, init, init_all};
+    dev::KArgs kc{out, flags, nullptr, lc.tables, nullptr, nullptr};
+    kc.raws = reinterpret_cast<uint32_t*>(ws);
+    const uint32_t gc = grid_for(lc.num_cu, T);
+    if (ev_start)
+      hipExtLaunchKernelGGL(dev::crc32c_chunks_kernel, dim3(gc), dim3(dev::kThreads), 0, lc.stream, ev_start, nullptr,
+                            0u, cg, kc);
+    else
+      hipLaunchKernelGGL(dev::crc32c_chunks_kernel, dim3(gc), dim3(dev::kThreads), 0, lc.stream, cg, kc);
+    hipError_t ec = hipGetLastError();
+    if (ec != hipSuccess) return ec;
+    const uint32_t G = (uint32_t)fold_segments(J);
+    uint32_t* segs = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ws) +
+                                                 (n * (uint64_t)J * sizeof(uint32_t) + 255u) / 256u * 256u);
+    dev::FoldSeg f1{kc.raws, n, J, kFoldSeg, G, 0u, {}, segs, flags};
+    fold_powers(dev::kChunk, kFoldSeg, &f1.step, f1.m);
+    dev::FoldSeg f2{segs, n, G, G, 1u, 0u, {}, out, flags};
+    fold_powers((uint64_t)dev::kChunk * kFoldSeg, G, &f2.step, f2.m);
+    const uint32_t g1 = (uint32_t)std::min<uint64_t>((n * G + 3) / 4, 65535);
+    hipLaunchKernelGGL(dev::crc32c_fold_seg_kernel, dim3(g1), dim3(256), 0, lc.stream, f1);
+    ec = hipGetLastError();
+    if (ec != hipSuccess) return ec;
+    const uint32_t g2 = (uint32_t)std::min<uint64_t>((n + 3) / 4, 65535);
+    if (lc.ev_stop)
+      hipExtLaunchKernelGGL(dev::crc32c_fold_seg_kernel, dim3(g2), dim3(256), 0, lc.stream, nullptr, lc.ev_stop, 0u, f2);
+    else
+      hipLaunchKernelGGL(dev::crc32c_fold_seg_kernel, dim3(g2), dim3(256), 0, lc.stream, f2);
+    return hipGetLastError();
+  }
   if (aligned && J > 1 && J <= kChunkParallelMaxJ) {
     const uint64_t T = n * (uint64_t)J;
     const uint32_t jsh = (J & (J - 1u)) == 0u ? (uint32_t)__builtin_ctz(J) : 64u;

@@ -102,11 +102,12 @@ def test_fixed_general_giant(dev, C, port, L, n, stride_gap, base_off):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("J,n", [(1025, 3), (262144, 1), (4096, 2)])
+@pytest.mark.parametrize("J,n", [(1025, 3), (2049, 2), (5127, 1), (262144, 1), (4096, 2)])
 def test_fixed_aligned_long_buffers(dev, C, port, J, n):
-    """Aligned fixed-stride batches of buffers longer than the chunk-parallel
-    fold takes (J > 1024 chunks: scheduler B, unit records, fix-up), incl. a
-    lone 1 GiB buffer, with per-buffer inits and Mask."""
+    """Aligned fixed-stride batches of buffers longer than the one-level
+    chunk fold takes (J > 1024 chunks: the two-level fold over segments of
+    1024 chunk raws, first segment clipped), incl. a lone 1 GiB buffer, with
+    per-buffer inits and Mask."""
     L = J * 4096
     host = port.fill(0xA1A + J, 0, n * L)
     buf = torch.from_numpy(host).to(dev)

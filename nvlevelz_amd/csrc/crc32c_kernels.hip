@@ -742,16 +742,115 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
 // keeps them hoisted (OPQ = false): since the general kernels stopped
 // spilling, hoisting costs no spill there and saves 22 us on config 3
 // (306 -> 285 us, same-box A/B).
-template <int U, bool OPQ>
+// The region kernel's LDS image: no butterfly tables.  Each lane moves its
+// piece raw to the chunk end by its OWN constant, x^(8*64*(63 - lane)), from
+// nibble tables T[n][v][lane] = shift(v << 4n, 64(63 - lane)) (8 x 16 rows of
+// 64 lanes: a lane reads only its own column, conflict-free); the chunk raw
+// and every lane prefix are then plain XORs over lanes (xor_scan, DPP).
+// Lane 63 (identity) never reads its column, whose first slot holds the
+// workgroup's unit counter.  The slice replicas follow at 32 KiB.
+constexpr uint32_t kRNibOff = 0;
+constexpr uint32_t kRCtrOff = 252;  // T[0][0][63]
+constexpr uint32_t kRSliceOff = 32768;
+constexpr uint32_t kRLdsBytes = kRSliceOff + kRepBytes;  // 163840 B
+static_assert(kRLdsBytes <= 160u * 1024u, "region LDS image exceeds 160 KiB");
+constexpr uint32_t kGNib = kTabNib;  // the blob's nibble tables (crc32c_internal.h)
+
+// The region image: slice replicas at kRSliceOff, nibble tables verbatim,
+// the unit counter patched into its slot by the thread that copies it.  In
+// two halves so that the blob loads are in flight together with the waves'
+// first searches (a fill after the search waited for both in turn: 6 us to
+// the first barrier).
+struct RegionFill {
+  uint32_t rep[8192 / kThreads];
+  uint4 nib[2048 / kThreads];
+};
+__device__ __forceinline__ RegionFill fill_region_load(const uint32_t* __restrict__ g) {
+  RegionFill f;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < (int)(8192 / kThreads); ++q) {
+    const uint32_t off = (uint32_t)(t + q * (int)kThreads) << 4;
+    const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
+    f.rep[q] = g[kGSlice + tab * 256u + ((off >> 8) & 0xFFu)];
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(g + kGNib);
+#pragma unroll
+  for (int q = 0; q < (int)(2048 / kThreads); ++q) f.nib[q] = src[t + q * (int)kThreads];
+  return f;
+}
+__device__ __forceinline__ void fill_region_store(uint8_t* lds, const RegionFill& f, uint32_t ctr0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < (int)(8192 / kThreads); ++q) {
+    const uint32_t off = (uint32_t)(t + q * (int)kThreads) << 4;
+    *reinterpret_cast<uint4*>(lds + kRSliceOff + off) = make_uint4(f.rep[q], f.rep[q], f.rep[q], f.rep[q]);
+  }
+  uint4* dst = reinterpret_cast<uint4*>(lds + kRNibOff);
+#pragma unroll
+  for (int q = 0; q < (int)(2048 / kThreads); ++q) {
+    uint4 v = f.nib[q];
+    if (t + q * (int)kThreads == (int)(kRCtrOff >> 4)) v.w = ctr0;  // units 0..ctr0-1 are pre-assigned
+    dst[t + q * (int)kThreads] = v;
+  }
+}
+static_assert(8192 % kThreads == 0 && 2048 % kThreads == 0, "region fill: whole rounds per thread");
+
+// shift(lr, 64(63 - lane)): this lane's piece raw moved to the chunk end.
+// Address of row (n, v): v << 8 | lane << 2 -- v_perm puts the nibble byte
+// over the lane byte; n is the ds_read immediate.
+__device__ __forceinline__ uint32_t to_chunk_end(const uint8_t* lds, uint32_t lr, uint32_t jb, int lane) {
+  const uint32_t lo = lr & 0x0F0F0F0Fu, hi = (lr >> 4) & 0x0F0F0F0Fu;
+  const uint8_t* nb = lds + kRNibOff;
+  const uint32_t r0 = lds_u32(nb + 0u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0400u));
+  const uint32_t r1 = lds_u32(nb + 1u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0400u));
+  const uint32_t r2 = lds_u32(nb + 2u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0500u));
+  const uint32_t r3 = lds_u32(nb + 3u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0500u));
+  const uint32_t r4 = lds_u32(nb + 4u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0600u));
+  const uint32_t r5 = lds_u32(nb + 5u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0600u));
+  const uint32_t r6 = lds_u32(nb + 6u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0700u));
+  const uint32_t r7 = lds_u32(nb + 7u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0700u));
+  const uint32_t t = xor3(xor3(r0, r1, r2), xor3(r3, r4, r5), r6) ^ r7;
+  return lane == 63 ? lr : t;
+}
+
+// Inclusive XOR scan over the wave's 64 lanes (rows of 16 by row_shr, then
+// row_bcast:15 / :31 across rows).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_or0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t xor_scan(uint32_t x) {
+  x ^= dpp_or0<0x111, 0xF>(x);  // row_shr:1
+  x ^= dpp_or0<0x112, 0xF>(x);  // row_shr:2
+  x ^= dpp_or0<0x114, 0xF>(x);  // row_shr:4
+  x ^= dpp_or0<0x118, 0xF>(x);  // row_shr:8
+  x ^= dpp_or0<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3
+  x ^= dpp_or0<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+
+// NIB: the region LDS image (slice replicas at kRSliceOff, nibble tables at
+// 0): each lane's piece raw moved to the chunk end by its own nibble-table
+// column and XOR-reduced over the wave (to_chunk_end + xor_scan) instead of
+// the byte-sliced butterfly -- fewer VALU per chunk.
+template <int U, bool OPQ, bool NIB = false>
 __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, const uint32_t (&w)[U][16], int lane,
                                        uint32_t (&raw)[U]) {
   uint32_t crc[U];
+  const uint8_t* sl = NIB ? lds + (kRSliceOff - kSliceOff) : lds;
 #pragma unroll
   for (int u = 0; u < U; ++u) crc[u] = w[u][0];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) crc[u] = slice4_next(lds, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+    for (int u = 0; u < U; ++u) crc[u] = slice4_next(sl, crc[u], k < 15 ? w[u][k + 1] : 0u, lb);
+  }
+  if constexpr (NIB) {
+    const uint32_t jb = (uint32_t)lane << 2;
+#pragma unroll
+    for (int u = 0; u < U; ++u) raw[u] = lane_u32(xor_scan(to_chunk_end(lds, crc[u], jb, lane)), 63u);
+    return;
   }
   // Lane = stream position P: lane bit k steps 64*2^k bytes (comb table k).
   // Bits 0 and 1 go first: afterwards the lanes of a quad hold equal values,
@@ -773,14 +872,14 @@ __device__ __forceinline__ void chains(const uint8_t* lds, const LaneBase& lb, c
 }
 
 // Raw (zero-state, ~init injected) registers of U chunks, wave-uniform.
-template <int M, int U>
+template <int M, int U, bool NIB = false>
 __device__ __forceinline__ void group_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo (&bi)[U],
                                           const uint32_t (&c)[U], int lane, const Chunk (&ch)[U],
                                           uint32_t (&raw)[U]) {
   uint32_t w[U][16], ov[4];
 #pragma unroll
   for (int u = 0; u < U; ++u) build_words<M>(bi[u], c[u], lane, ch[u], w[u], ov);
-  chains<U, false>(lds, lb, w, lane, raw);
+  chains<U, false, NIB>(lds, lb, w, lane, raw);
 }
 
 // Chain + butterfly of one chunk from its built words.
@@ -794,14 +893,14 @@ __device__ __forceinline__ uint32_t chain_fold(const uint8_t* lds, const LaneBas
   return r[0];
 }
 
-template <int M>
+template <int M, bool NIB = false>
 __device__ __forceinline__ uint32_t chunk_raw(const uint8_t* lds, const LaneBase& lb, const BufInfo& bi,
                                               uint32_t c, int lane, const Chunk& ch) {
   const BufInfo b1[1] = {bi};
   const uint32_t c1[1] = {c};
   const Chunk h1[1] = {ch};
   uint32_t r1[1];
-  group_raw<M, 1>(lds, lb, b1, c1, lane, h1, r1);
+  group_raw<M, 1, NIB>(lds, lb, b1, c1, lane, h1, r1);
   return r1[0];
 }
 
@@ -910,7 +1009,7 @@ __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane, uint32_t c
 #endif
 constexpr uint32_t kTail = NVL_TAIL;
 
-template <int U, int NW = kWavesPerWG, int M = kAligned, class G = FixedGeom, bool kRaw = false>
+template <int U, int NW = kWavesPerWG, int M = kAligned, class G = FixedGeom, bool kRaw = false, bool NIB = false>
 __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
   const int lane = threadIdx.x & 63;
@@ -941,14 +1040,15 @@ __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* 
     ok[k] = unit_pos(u, k, gp[k]);
     if (ok[k]) load_chunk<M>(gp[k].bi, 0, lane, cur[k]);
   }
-  fill_lds<NW>(lds, ka.tables);
+  if constexpr (NIB) fill_region_store(lds, fill_region_load(ka.tables), NW);
+  else fill_lds<NW>(lds, ka.tables);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();
 
   while (u < nunits) {
     NVL_COUNT();
-    const uint32_t un = pull_unit(lds, lane);
+    const uint32_t un = pull_unit(lds, lane, NIB ? kRCtrOff : kCtrOff);
     Pos np[U];
     bool nok[U];
     Chunk nxt[U];
@@ -965,7 +1065,7 @@ __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* 
         bis[k] = gp[k].bi;
         cs[k] = 0;
       }
-      group_raw<M, U>(lds, lb, bis, cs, lane, cur, raws);
+      group_raw<M, U, NIB>(lds, lb, bis, cs, lane, cur, raws);
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -977,7 +1077,7 @@ __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* 
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         if (ok[k]) {
-          const uint32_t r = chunk_raw<M>(lds, lb, gp[k].bi, 0, lane, cur[k]);
+          const uint32_t r = chunk_raw<M, NIB>(lds, lb, gp[k].bi, 0, lane, cur[k]);
           if (lane == 0) {
             if constexpr (kRaw) ka.raws[gp[k].i] = r;
             else ka.out[gp[k].i] = finish(~r, ka.flags);
@@ -2083,11 +2183,14 @@ template <int M>
 constexpr int waves_of() { return M == kGeneral ? kGenWaves : kWavesPerWG; }
 
 template <int M>
+#ifndef NVL_FIXED_NIB
+#define NVL_FIXED_NIB 1  // 1: config 2's chunks fold through the nibble lane shifts (chains<NIB>)
+#endif
 __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes > kRLdsBytes ? kLdsBytes : kRLdsBytes];
   if constexpr (M == kAligned) {
     if (g.J == 1) {
-      run_pairs<NVL_FAST_U>(g, ka, lds);
+      run_pairs<NVL_FAST_U, kWavesPerWG, kAligned, FixedGeom, false, NVL_FIXED_NIB != 0>(g, ka, lds);
       return;
     }
   }
@@ -2120,8 +2223,8 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
 // Aligned multi-chunk fixed batches (config 4): every 4 KiB chunk an
 // independent scheduler-A pass (ChunkGeom), raw registers to KArgs::raws.
 __global__ __launch_bounds__(kThreads, 1) void crc32c_chunks_kernel(ChunkGeom g, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  run_pairs<NVL_FAST_U, kWavesPerWG, kAligned, ChunkGeom, true>(g, ka, lds);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes > kRLdsBytes ? kLdsBytes : kRLdsBytes];
+  run_pairs<NVL_FAST_U, kWavesPerWG, kAligned, ChunkGeom, true, NVL_FIXED_NIB != 0>(g, ka, lds);
 }
 
 // Buffer i of J chunks: raw = XOR_c shift(raws[iJ + c], 4096 (J - 1 - c)).
@@ -2881,94 +2984,6 @@ __device__ uint64_t region_search(const RegionGeom& g, uint64_t A, int lane, con
   const uint64_t e = g.rel0 + ldg64(g.offsets, bc) + ldg64(g.lengths, bc);
   const uint64_t m = __ballot(b < hi && e > A);
   return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
-}
-
-// The region kernel's LDS image: no butterfly tables.  Each lane moves its
-// piece raw to the chunk end by its OWN constant, x^(8*64*(63 - lane)), from
-// nibble tables T[n][v][lane] = shift(v << 4n, 64(63 - lane)) (8 x 16 rows of
-// 64 lanes: a lane reads only its own column, conflict-free); the chunk raw
-// and every lane prefix are then plain XORs over lanes (xor_scan, DPP).
-// Lane 63 (identity) never reads its column, whose first slot holds the
-// workgroup's unit counter.  The slice replicas follow at 32 KiB.
-constexpr uint32_t kRNibOff = 0;
-constexpr uint32_t kRCtrOff = 252;  // T[0][0][63]
-constexpr uint32_t kRSliceOff = 32768;
-constexpr uint32_t kRLdsBytes = kRSliceOff + kRepBytes;  // 163840 B
-static_assert(kRLdsBytes <= 160u * 1024u, "region LDS image exceeds 160 KiB");
-constexpr uint32_t kGNib = kTabNib;  // the blob's nibble tables (crc32c_internal.h)
-
-// The region image: slice replicas at kRSliceOff, nibble tables verbatim,
-// the unit counter patched into its slot by the thread that copies it.  In
-// two halves so that the blob loads are in flight together with the waves'
-// first searches (a fill after the search waited for both in turn: 6 us to
-// the first barrier).
-struct RegionFill {
-  uint32_t rep[8192 / kThreads];
-  uint4 nib[2048 / kThreads];
-};
-__device__ __forceinline__ RegionFill fill_region_load(const uint32_t* __restrict__ g) {
-  RegionFill f;
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < (int)(8192 / kThreads); ++q) {
-    const uint32_t off = (uint32_t)(t + q * (int)kThreads) << 4;
-    const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
-    f.rep[q] = g[kGSlice + tab * 256u + ((off >> 8) & 0xFFu)];
-  }
-  const uint4* src = reinterpret_cast<const uint4*>(g + kGNib);
-#pragma unroll
-  for (int q = 0; q < (int)(2048 / kThreads); ++q) f.nib[q] = src[t + q * (int)kThreads];
-  return f;
-}
-__device__ __forceinline__ void fill_region_store(uint8_t* lds, const RegionFill& f, uint32_t ctr0) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < (int)(8192 / kThreads); ++q) {
-    const uint32_t off = (uint32_t)(t + q * (int)kThreads) << 4;
-    *reinterpret_cast<uint4*>(lds + kRSliceOff + off) = make_uint4(f.rep[q], f.rep[q], f.rep[q], f.rep[q]);
-  }
-  uint4* dst = reinterpret_cast<uint4*>(lds + kRNibOff);
-#pragma unroll
-  for (int q = 0; q < (int)(2048 / kThreads); ++q) {
-    uint4 v = f.nib[q];
-    if (t + q * (int)kThreads == (int)(kRCtrOff >> 4)) v.w = ctr0;  // units 0..ctr0-1 are pre-assigned
-    dst[t + q * (int)kThreads] = v;
-  }
-}
-static_assert(8192 % kThreads == 0 && 2048 % kThreads == 0, "region fill: whole rounds per thread");
-
-// shift(lr, 64(63 - lane)): this lane's piece raw moved to the chunk end.
-// Address of row (n, v): v << 8 | lane << 2 -- v_perm puts the nibble byte
-// over the lane byte; n is the ds_read immediate.
-__device__ __forceinline__ uint32_t to_chunk_end(const uint8_t* lds, uint32_t lr, uint32_t jb, int lane) {
-  const uint32_t lo = lr & 0x0F0F0F0Fu, hi = (lr >> 4) & 0x0F0F0F0Fu;
-  const uint8_t* nb = lds + kRNibOff;
-  const uint32_t r0 = lds_u32(nb + 0u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0400u));
-  const uint32_t r1 = lds_u32(nb + 1u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0400u));
-  const uint32_t r2 = lds_u32(nb + 2u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0500u));
-  const uint32_t r3 = lds_u32(nb + 3u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0500u));
-  const uint32_t r4 = lds_u32(nb + 4u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0600u));
-  const uint32_t r5 = lds_u32(nb + 5u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0600u));
-  const uint32_t r6 = lds_u32(nb + 6u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0700u));
-  const uint32_t r7 = lds_u32(nb + 7u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0700u));
-  const uint32_t t = xor3(xor3(r0, r1, r2), xor3(r3, r4, r5), r6) ^ r7;
-  return lane == 63 ? lr : t;
-}
-
-// Inclusive XOR scan over the wave's 64 lanes (rows of 16 by row_shr, then
-// row_bcast:15 / :31 across rows).
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp_or0(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
-}
-__device__ __forceinline__ uint32_t xor_scan(uint32_t x) {
-  x ^= dpp_or0<0x111, 0xF>(x);  // row_shr:1
-  x ^= dpp_or0<0x112, 0xF>(x);  // row_shr:2
-  x ^= dpp_or0<0x114, 0xF>(x);  // row_shr:4
-  x ^= dpp_or0<0x118, 0xF>(x);  // row_shr:8
-  x ^= dpp_or0<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3
-  x ^= dpp_or0<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
-  return x;
 }
 
 // Chains of U chunks, then per chunk: raw[u] = raw(0, chunk) (wave-uniform)

@@ -3177,7 +3177,7 @@ __device__ __forceinline__ uint32_t fold_sh4096(const uint32_t* sh, uint32_t acc
 // caller then checksums the buffer serially.
 struct FoldIn {
   uint64_t s, L;
-  uint32_t ninit, xs, xe, xt;  // x^(8(4096 - os)), x^(-8(4096 - oe)), x^(8L) (one chunk) / x^(8(8192 - os)) (two)
+  uint32_t ninit, xs, xe, xt;  // x^(8(4096 - os)), x^(-8(4096 - oe)), x^(8L) (one or two chunks)
   u32x4 vs, ve;
   bool fast;  // inside the region, >= kRegionDirect bytes, every chunk streamed by this workgroup
 };
@@ -3198,7 +3198,7 @@ __device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* t
   f.xs = tables[kTabXp8 + kChunk - os];
   f.xe = tables[kTabXm8 + (kChunk - oe)];
   const uint64_t c0 = s >> 12;
-  f.xt = tables[kTabXp8 + (c1 == c0 ? e - s : (c1 == c0 + 1u ? 2u * kChunk - os : 0u))];
+  f.xt = tables[kTabXp8 + (c1 <= c0 + 1u ? e - s : 0u)];  // (L <= 8192 there)
   return f;
 }
 
@@ -3279,16 +3279,14 @@ __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds
   const uint32_t T = (os ? quad_prefix_lds(lsl, lb, q_s.y, f.vs, s & 63u) : 0u) ^ f.ninit;  // R(s) ^ ~init, at s
   const uint32_t ze = oe == kChunk ? r1 : q_e.x;                         // chunk c1's bytes before e, at its end
   const uint32_t re = oe == kChunk ? 0u : quad_prefix_lds(lsl, lb, q_e.y, f.ve, e & 63u);  // R(e), at e
-  if (c1 == c0) {  // one chunk: (Ze ^ Qe(s)) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e), two independent multiplies
-    v = gf_mul_lds(lsl, lb, f.xe, ze ^ qs) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ re;
-    return true;
-  }
-  if (c1 == c0 + 1u) {
-    // two chunks, everything at chunk c1's end, then one unshift:
-    //   (shift4096(Qe(s) ^ raw c0) ^ T x^(8(8192 - os)) ^ Ze) x^(-8(4096 - oe)) ^ R(e)
-    // (two multiplies and two column shifts: the fold is VALU-bound, and a
-    // third multiply in parallel cost more than the longer chain)
-    v = gf_mul_lds(lsl, lb, f.xe, sh4096_lds(lds, qs ^ r0, lane) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ ze) ^ re;
+  if (c1 <= c0 + 1u) {
+    // one or two chunks, one formula (a slice holding both kinds would run
+    // both branches): the data terms at chunk c1's end -- Qe(s) (one chunk)
+    // or shift4096(Qe(s) ^ raw c0) (two) -- ^ Ze, unshifted to e, and T
+    // straight to e:  (X ^ Ze) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e)
+    // (for two chunks x^(-8(4096 - oe)) x^(8(8192 - os)) = x^(8L))
+    const uint32_t sh = sh4096_lds(lds, qs ^ r0, lane);
+    v = gf_mul_lds(lsl, lb, f.xe, (c1 == c0 ? qs : sh) ^ ze) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ re;
     return true;
   }
   // Longer: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) at chunk c0's end, the chunks in between, unshifted from c1's end
@@ -3316,7 +3314,10 @@ __device__ __forceinline__ lds_vu32* region_slot(uint8_t* lds, uint32_t r) {
   return (lds_vu32*)(lds + kRNibOff + r * 256u + 252u);
 }
 constexpr uint32_t kSlotOwnLo = 1, kSlotOwnHi = 2, kSlotEndLo = 3, kSlotEndHi = 4, kSlotHalo = 5;
-constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32: T[1][0][63], T[2][0][63] = 0 in the blob)
+constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32, 48, 64, 80: T[n][0][63] = 0 in the blob)
+#ifndef NVL_FOLD_SIMD
+#define NVL_FOLD_SIMD 1
+#endif
 
 // Scheduler A over the region's chunks, and the per-buffer fold in the same
 // launch.  Workgroup b owns the chunk range [B0, B1) and the buffers
@@ -3335,6 +3336,11 @@ constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32: T[1][0][63
 // without its records or with chunks outside the workgroup's streamed range
 // is checksummed serially (unsorted or overlapping batches: correct, slow).
 // Buffers must lie inside the region (the entry point's contract).
+#ifndef NVL_RTAIL
+#define NVL_RTAIL 16
+#endif
+constexpr uint32_t kRTail = NVL_RTAIL;  // single-chunk units at the end of a range
+
 template <int U>
 __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds) {
   NVL_TL_DECL();
@@ -3344,7 +3350,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint64_t B0 = g.nc * blockIdx.x / gridDim.x;
   const uint64_t B1 = g.nc * (blockIdx.x + 1) / gridDim.x;
   const uint32_t cnt = (uint32_t)(B1 - B0);
-  const uint32_t nfull = cnt > kTail ? (cnt - kTail) / U : 0u;
+  const uint32_t nfull = cnt > kRTail ? (cnt - kRTail) / U : 0u;
   const uint32_t nunits = nfull + (cnt - nfull * U);
   uint64_t C0 = B0;       // the halo's first chunk (B0: none) -- known once wave 0 published it
   uint32_t nhalo = ~0u;   // halo units, ~0u until read
@@ -3529,6 +3535,18 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint64_t ib1 = ((uint64_t)*region_slot(lds, kSlotEndHi) << 32) | *region_slot(lds, kSlotEndLo);
   const uint64_t c0w = B0 - *region_slot(lds, kSlotHalo);  // the first chunk streamed here
   const uint64_t nsl = ib1 > ib ? (ib1 - ib + 63u) / 64u : 0u;
+#if NVL_FOLD_SIMD
+  // slices k = simd (mod 4) to this wave's SIMD (HW_ID bits 5:4): the fold
+  // is VALU-bound, so a SIMD holding two folding waves finishes last
+  const uint32_t simd = uniform_u32(__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u);
+  auto claim = [&]() -> uint64_t {
+    uint32_t v = 0;
+    if (lane == 0)
+      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail + 16u * simd)), 1u,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (uint64_t)simd + 4u * (uint64_t)uniform_u32(v);
+  };
+#else
   auto claim = [&]() -> uint64_t {
     uint32_t v = 0;
     if (lane == 0)
@@ -3536,6 +3554,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return uniform_u32(v);
   };
+#endif
   uint64_t k = claim();
   FoldIn f;
   if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);

@@ -500,9 +500,10 @@ def region_fold(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
 
 def region_fold_direct(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     """The region kernel's fold as it computes a buffer spanning at most two
-    chunks (one chunk: every term moved straight to e, two independent
-    multiplies; two chunks: every term at chunk c1's end, one unshift).
-    Longer buffers: region_fold."""
+    chunks, one formula for both (no divergence in a wave that holds both):
+    the data terms at chunk c1's end -- Qe(s) directly (one chunk) or
+    shift4096(Qe(s) ^ raw c0) (two) -- unshifted to e, plus T x^(8L) and
+    R(e): two independent multiplies.  Longer buffers: region_fold."""
     if L < REGION_DIRECT:
         return (~raw_bytes((~init) & 0xFFFFFFFF, mem[s:s + L])) & 0xFFFFFFFF
     e = s + L
@@ -516,10 +517,8 @@ def region_fold_direct(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     ze = raws[c1] if oe == 4096 else qe[("e", c1, oe)]
     re = 0 if oe == 4096 else piece_prefix_raw(mem, e)
     back = lambda v: unshift(v, 4096 - oe)  # x^(-8(4096 - oe))
-    if c1 == c0 + 1:
-        v = back(apply_op(SH4096, qs ^ raws[c0]) ^ shift(T, 8192 - os_) ^ ze) ^ re
-    else:
-        v = back(ze ^ qs) ^ shift(T, L) ^ re
+    X = apply_op(SH4096, qs ^ raws[c0]) if c1 == c0 + 1 else qs
+    v = back(X ^ ze) ^ shift(T, L) ^ re
     return (~v) & 0xFFFFFFFF
 
 

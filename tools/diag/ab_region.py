@@ -50,12 +50,18 @@ def run(k):
                                             st)
     return libs[k].nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.data_ptr(), None, 0,
                                          outs[k].data_ptr(), n, 0, ws.data_ptr(), wsb, st)
-rounds, reps = int(os.environ.get("AB_ROUNDS", "6")), int(os.environ.get("AB_REPS", "30"))
+rounds, reps = int(os.environ.get("AB_ROUNDS", "10")), int(os.environ.get("AB_REPS", "30"))
 per = [[] for _ in range(len(libs) + 1)]
 single = [[] for _ in range(len(libs) + 1)]
 for k in range(len(libs) + 1):
     for _ in range(5): run(k)
 torch.cuda.synchronize()
+import time
+t0 = time.perf_counter()  # ~100 ms of load first: the GPU's sustained-load state (the first ~30 ms run slower)
+while time.perf_counter() - t0 < 0.1:
+    for k in range(len(libs) + 1):
+        for _ in range(5): run(k)
+    torch.cuda.synchronize()
 for r in range(rounds):
     for k in range(len(libs) + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -40,6 +40,7 @@ run = lambda: lib.nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.d
                                         0, ws.data_ptr(), wsb, st)
 reps = int(os.environ.get("REPS", "5"))
 res = []
+lastx = []
 for r in range(reps + 3):
     for _ in range(20): run()  # back to back, as in the sustained measurement; stamps of the last call
     torch.cuda.synchronize()
@@ -59,10 +60,17 @@ for r in range(reps + 3):
     q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 50, 90, 100)]
     f0 = wg[:, :, 4] > 0  # waves that folded a slice: records in (4), arithmetic done (5)
     rec = (wg[:, :, 4] - wg[:, :, 3])[f0]; ari = (wg[:, :, 5] - wg[:, :, 4])[f0]; sto = (wg[:, :, 7] - wg[:, :, 5])[f0]
-    res.append({"search_done_us": q(wg[:, :, 6].max(1)), "fold_records_us": q(rec), "fold_arith_us": q(ari), "fold_store_exit_us": q(sto),
+    lastx.append(loop_last - loop_last.mean())
+    xcd = [round(float(np.median(loop_last[x::8] - loop_last.mean())), 2) for x in range(8)]
+    res.append({"wg_last_exit_by_xcd_us": xcd, "search_done_us": q(wg[:, :, 6].max(1)), "fold_records_us": q(rec), "fold_arith_us": q(ari), "fold_store_exit_us": q(sto),
                 "kernel_end_us": round(float(us[:, 7].max()), 2), "last_out_of_units_us": round(float(loop_last.max()), 2),
                 "fill_barrier_us": q(wg[:, :, 1].max(1)), "wg_unit_exit_spread_us": q(loop_last - loop_first),
                 "wg_barrier_after_last_exit_us": q(bar - loop_last), "wg_fold_us": q(end - bar),
                 "wg_end_us": q(end), "wg_last_exit_us": q(loop_last)})
 for r in res:
     print(json.dumps(r), flush=True)
+L = np.array(lastx)  # reps x G: is a slow workgroup slow every time?
+cc = np.corrcoef(L)
+print(json.dumps({"wg_last_exit_rep_corr": [round(float(cc[i, i + 1]), 3) for i in range(len(L) - 1)],
+                  "wg_last_exit_std_us": round(float(L.std(1).mean()), 2),
+                  "wg_last_exit_mean_over_reps_std_us": round(float(L.mean(0).std()), 2)}), flush=True)

@@ -12,6 +12,13 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   --master-port 29531 bench.py --gpus 2 --steps 50 --warmup 10 --no-cpu > $OUT/dist_n2.json 2> $OUT/dist_n2.err
 rc=$?; echo "[dist] n2 rc=$rc"; cat $OUT/dist_n2.json
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --gpus 4 --steps 50 --warmup 10 --no-cpu > $OUT/dist_n4.json 2> $OUT/dist_n4.err
+rc=$?; echo "[dist] n4 (self-spawned ranks) rc=$rc"; cat $OUT/dist_n4.json
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 8 --steps 50 --warmup 10 --no-cpu > $OUT/dist_n8.json 2> $OUT/dist_n8.err
+rc=$?; echo "[dist] n8 rc=$rc"; cat $OUT/dist_n8.json
+[ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
   --master-port 29532 bench.py --gpus 4 --config cfg5 --steps 5 --warmup 2 --no-cpu > $OUT/dist_n4_cfg5.json 2> $OUT/dist_n4_cfg5.err
 rc=$?; echo "[dist] n4 cfg5 rc=$rc"; cat $OUT/dist_n4_cfg5.json

@@ -3342,7 +3342,7 @@ constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32, 48, 64, 80
 // is checksummed serially (unsorted or overlapping batches: correct, slow).
 // Buffers must lie inside the region (the entry point's contract).
 #ifndef NVL_RTAIL
-#define NVL_RTAIL 16
+#define NVL_RTAIL 8
 #endif
 constexpr uint32_t kRTail = NVL_RTAIL;  // single-chunk units at the end of a range
 

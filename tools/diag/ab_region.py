@@ -63,7 +63,8 @@ while time.perf_counter() - t0 < 0.1:
         for _ in range(5): run(k)
     torch.cuda.synchronize()
 for r in range(rounds):
-    for k in range(len(libs) + 1):
+    ks = list(range(len(libs) + 1))
+    for k in ks[r % len(ks):] + ks[:r % len(ks)]:  # (rotated each round: no variant always follows the same one)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps): run(k)

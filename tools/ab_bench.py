@@ -19,7 +19,7 @@ def load(path):
 def main():
     paths = sys.argv[1:]
     n = int(os.environ.get("AB_BLOCKS", "100000")); L = int(os.environ.get("AB_LEN", "4096"))
-    rounds = int(os.environ.get("AB_ROUNDS", "8")); reps = int(os.environ.get("AB_REPS", "20"))
+    rounds = int(os.environ.get("AB_ROUNDS", "12")); reps = int(os.environ.get("AB_REPS", "20"))
     dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
     libs = [load(p) for p in paths]
     for lib in libs:
@@ -38,8 +38,22 @@ def main():
     for k in range(len(libs)):
         for _ in range(3): run(k)
     torch.cuda.synchronize()
-    for r in range(rounds):
+    t0 = time.perf_counter()  # ~100 ms of load first: the sustained-load state (the first ~30 ms run slower)
+    while time.perf_counter() - t0 < 0.1:
         for k in range(len(libs)):
+            for _ in range(5): run(k)
+        torch.cuda.synchronize()
+    periods = [[] for _ in libs]
+    for r in range(rounds):
+        ks = list(range(len(libs)))
+        for k in ks[r % len(ks):] + ks[:r % len(ks)]:  # (rotated: no variant always follows the same one)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for j in range(reps):
+                run(k)
+            e1.record()
+            torch.cuda.synchronize()
+            periods[k].append(e0.elapsed_time(e1) * 1e3 / reps)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
             for j in range(reps):
                 ev[2*j].record(); run(k); ev[2*j+1].record()
@@ -57,6 +71,7 @@ def main():
         print(json.dumps({"variant": os.path.basename(p), "median_us": round(float(np.median(t)), 2),
                           "min_us": round(float(t.min()), 2), "GB/s": round(gbs, 1), "frac": round(gbs / 8000, 4),
                           "wall_us_per_step": round(float(np.median(walls[k])), 2),
+                          "period_us": round(float(np.median(periods[k])), 2),
                           "same_as_first": same}))
 
 main()

@@ -61,6 +61,14 @@ for r in range(reps + 3):
     f0 = wg[:, :, 4] > 0  # waves that folded a slice: records in (4), arithmetic done (5)
     rec = (wg[:, :, 4] - wg[:, :, 3])[f0]; ari = (wg[:, :, 5] - wg[:, :, 4])[f0]; sto = (wg[:, :, 7] - wg[:, :, 5])[f0]
     lastx.append(loop_last - loop_last.mean())
+    entry = wg[:, :, 0].min(1)  # workgroup dispatch (its first wave's entry)
+    bi = np.arange(G)
+    ent_xcd = [round(float(np.median(entry[x::8])), 2) for x in range(8)]
+    print(json.dumps({"wg_entry_us": q(entry), "entry_by_xcd_us": ent_xcd,
+                      "entry_slope_us_per_wg": round(float(np.polyfit(bi, entry, 1)[0]), 4),
+                      "corr_entry_lastexit": round(float(np.corrcoef(entry, loop_last)[0, 1]), 3),
+                      "corr_entry_unitwork": round(float(np.corrcoef(entry, loop_last - entry)[0, 1]), 3),
+                      "lastexit_minus_entry_us": q(loop_last - entry)}), flush=True)
     xcd = [round(float(np.median(loop_last[x::8] - loop_last.mean())), 2) for x in range(8)]
     res.append({"wg_last_exit_by_xcd_us": xcd, "search_done_us": q(wg[:, :, 6].max(1)), "fold_records_us": q(rec), "fold_arith_us": q(ari), "fold_store_exit_us": q(sto),
                 "kernel_end_us": round(float(us[:, 7].max()), 2), "last_out_of_units_us": round(float(loop_last.max()), 2),

@@ -3551,7 +3551,10 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint64_t nsl = ib1 > ib ? (ib1 - ib + 63u) / 64u : 0u;
 #if NVL_FOLD_SIMD
   // slices k = simd (mod 4) to this wave's SIMD (HW_ID bits 5:4): the fold
-  // is VALU-bound, so a SIMD holding two folding waves finishes last
+  // is VALU-bound, so a SIMD holding two folding waves finishes last.  Every
+  // slice is claimed because every SIMD holds 4 of the 16 waves: at > 64
+  // VGPRs a SIMD takes at most 4 (tests/test_kernel_resources.py pins that;
+  // a fallback to the other SIMDs' counters measured 0.85 us slower on v)
   const uint32_t simd = uniform_u32(__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u);
   auto claim = [&]() -> uint64_t {
     uint32_t v = 0;

@@ -61,3 +61,15 @@ def test_no_vgpr_spills(usage, name):
         assert u.get("VGPRs Spill", 0) == 0, (k, u)
         assert u.get("SGPRs Spill", 0) <= SGPR_SPILL_MAX.get(name, 16), (k, u)
         assert u.get("ScratchSize", 0) <= 32, (k, u)  # a small indexed private array, no spill area
+
+
+def test_region_fold_claim_placement(usage):
+    """The region fold deals its slices by SIMD (slice k to a wave on SIMD
+    k mod 4, crc32c_kernels.hip run_region): every slice is claimed only if
+    every SIMD holds some of the workgroup's 16 waves, which the register
+    budget guarantees -- above 64 VGPRs a SIMD (512 per lane) takes at most 4
+    waves, so the 16 waves sit 4 per SIMD."""
+    hits = [k for k in usage if "crc32c_region_kernel" in k]
+    assert hits
+    for k in hits:
+        assert usage[k].get("VGPRs", 0) > 64, (k, usage[k])

@@ -31,6 +31,11 @@ The JSON line adds
                   PMC-measured HBM bytes per launch (profiles/pmc_traffic.json,
                   rocprofv3 --pmc passes, corrected per MI355X_MICROARCH.md
                   §HBM), labelled as such, else null.
+  cfg5         -- BASELINE config 5 on the same N ranks (every run, N = 1
+                  included): 10^7 x 4 KiB blocks in total round-robin over
+                  the N GPUs (strong scaling), its GiB/s, frac, and every
+                  rank's digest verified (cfg5_leg).  The headline `value`
+                  stays config 2 (weak scaling: N = 1 is BASELINE config 2).
   cpu_baseline -- the reference's own util/crc32c.cc + port/port_posix_sse.cc
                   (oracle/_ref, kind "reference"; the clean-room port, kind
                   "port", if _ref is absent) timed on this host's cores on a
@@ -67,6 +72,10 @@ def parse():
                     help="target seconds per CPU-baseline leg (all-core and 1-thread)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the all-core CPU leg (0 = every physical core this process may run on)")
+    ap.add_argument("--cfg5-steps", type=int, default=20,
+                    help="timed steps of the BASELINE config-5 leg (10^7 blocks in total, round-robin over the N "
+                         "GPUs, strong scaling) reported beside the headline; 0 = skip")
+    ap.add_argument("--cfg5-warmup", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host end-to-end leg (N=1)")
     ap.add_argument("--shims", action="store_true",
@@ -331,6 +340,74 @@ def shim_bench(nblocks: int = 100_000) -> dict:
     return res
 
 
+CFG5_BLOCKS = 10_000_000
+
+
+def cfg5_leg(steps: int, warmup: int, rank: int, world: int, dev, red_dev, golden: dict) -> dict:
+    """BASELINE config 5 beside the headline, on every `--gpus N` run (N = 1
+    included): 10^7 x 4 KiB blocks IN TOTAL, round-robin over the N ranks
+    (strong scaling: rank r holds global blocks r, r + N, ...; 41 GB at N = 1,
+    5.1 GB per GPU at N = 8), generated in place, one nvl_crc32c_fixed_dev
+    launch per step per rank, no data-path collective.  Every rank's CRCs are
+    verified before the timing (its own digest against the reference-built
+    per-rank golden, then the gathered global digest: shard.verify_shards,
+    tests/golden/configs.json cfg5.ranks).  Timed like the headline: barrier +
+    synchronize around `steps` back-to-back launches, MAX wall time over
+    ranks; the per-rank kernel period from HIP events on the launch stream."""
+    import torch
+    import torch.distributed as dist
+
+    from nvlevelz_amd import crc32c, shard
+
+    n_local = shard.local_count(CFG5_BLOCKS, rank, world)
+    buf = torch.empty(max(n_local, 1) * BLOCK, dtype=torch.uint8, device=dev)
+    crc32c.fill_splitmix(buf, n_local, BLOCK, SEED_CFG5, first_block=rank, block_step=world)
+    stream = torch.cuda.current_stream(dev)
+    batch = crc32c.FixedBatch(buf, BLOCK, BLOCK, n_local, stream=stream)
+    batch.launch()
+    torch.cuda.synchronize()
+    expect = shard.round_robin_expect(golden["cfg5"], world)
+    if world > 1:
+        v = shard.verify_shards(batch.out[:n_local].to(red_dev), CFG5_BLOCKS, expect)
+    else:
+        v = shard.verify_local(crc32c.to_u32(batch.out[:n_local]), expect)
+    for _ in range(warmup):
+        batch.launch()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        batch.launch()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    period_s = ev0.elapsed_time(ev1) / 1e3 / steps
+    frac = n_local * (BLOCK + 4) / period_s / 1e9 / HBM_PEAK_GBS
+    frac_min = frac
+    if world > 1:
+        t = torch.tensor([elapsed, -frac], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, frac_min = float(t[0].item()), -float(t[1].item())
+    del batch, buf
+    torch.cuda.empty_cache()
+    return {"workload": f"cfg5: 10^7 x 4 KiB blocks in total (BASELINE config 5), round-robin over {world} GPU(s), "
+                        f"device-resident, generated in place",
+            "value": round(CFG5_BLOCKS * BLOCK * steps / elapsed / 2**30, 3), "unit": "GiB/s",
+            "scaling": "strong", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "blocks_per_gpu_max": shard.local_count(CFG5_BLOCKS, 0, world),
+            "frac": round(frac, 4), "frac_min_over_ranks": round(frac_min, 4),
+            "mean_kernel_us_rank0": round(period_s * 1e6, 2),
+            "frac_what": "rank 0's alg bytes (its blocks x (4096 + 4)) / its kernel period (HIP events around the "
+                         "timed launches / steps) / 8 TB/s; frac_min_over_ranks the slowest rank's",
+            "verify": v}
+
+
 def main():
     args = parse()
     from nvlevelz_amd import launch  # (loads nothing: safe before the ranks exist)
@@ -520,6 +597,10 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    c5 = None
+    if args.config == "cfg2" and args.cfg5_steps > 0:  # BASELINE config 5 beside the cfg2 headline (all ranks)
+        c5 = cfg5_leg(args.cfg5_steps, args.cfg5_warmup, rank, N, dev, red_dev, golden)
+
     cpu = None
     e2e = None
     if rank == 0 and N == 1 and not args.no_cpu:
@@ -596,6 +677,8 @@ def main():
                         "what": "untimed diagnostic after the timed region: back-to-back launches, HIP events every "
                                 "100; frac over the whole run (the timed window's frac is roofline.frac)"})
             line["roofline"]["sustained"] = sus
+        if c5:
+            line["cfg5"] = c5
         if e2e:
             line["e2e"] = e2e
         if args.shims and N == 1:

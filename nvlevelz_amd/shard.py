@@ -61,6 +61,35 @@ def digest(crcs: np.ndarray) -> int:
     return crc32c.value(np.ascontiguousarray(crcs, dtype="<u4").view(np.uint8))
 
 
+def round_robin_expect(entry: dict, world: int) -> dict:
+    """verify_shards' expectations for `world` ranks from a golden entry of a
+    round-robin batch: the global "digest" / "crc_last", and each rank's own
+    digest from entry["ranks"][str(world)]["rank_digests"] (config 5,
+    tests/golden/configs.json; at world 1 the rank digest is the digest)."""
+    exp = {"digest": entry["digest"]}
+    if "crc_last" in entry:
+        exp["crc_last"] = entry["crc_last"]
+    if world == 1:
+        exp["rank_digests"] = [entry["digest"]]
+    else:
+        r = entry.get("ranks", {}).get(str(world))
+        if r is not None:
+            exp["rank_digests"] = list(r["rank_digests"])
+    return exp
+
+
+def verify_local(crcs: np.ndarray, expect: dict) -> dict:
+    """verify_shards' report for one rank holding the whole batch (N = 1, no
+    process group)."""
+    d = digest(crcs)
+    out = {"rank_digests_ok": d == expect["rank_digests"][0] if expect.get("rank_digests") else None,
+           "digest": hex(d), "digest_ok": d == expect["digest"], "blocks_checked": int(crcs.size),
+           "crc0": hex(int(crcs[0])) if crcs.size else None}
+    if "crc_last" in expect and crcs.size:
+        out["crc_last_ok"] = int(crcs[-1]) == expect["crc_last"]
+    return out
+
+
 def verify_shards(local, n_total: int, expect: dict, group=None) -> dict:
     """Check every rank's CRCs of a round-robin batch (outside any timed
     region).  local: this rank's int32 CRC tensor in local order; expect:

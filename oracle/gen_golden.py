@@ -259,12 +259,17 @@ def cfg5() -> dict:
             assert np.array_equal(crc[s:s + chunk], want), f"restatement != reference on chunk {k}"
             ref_checked += chunk
     sub = [p.digest(crc[s:s + 1_000_000]) for s in range(0, n, 1_000_000)]
+    # bench.py --gpus N's cfg5 leg: rank r holds blocks r, r + N, ... (round
+    # robin); each rank checks its own digest over its CRCs in local order
+    # (shard.verify_shards), rank 0 the gathered global one
+    ranks = {str(N): {"rank_digests": [p.digest(crc[k::N]) for k in range(N)]} for N in (2, 3, 4, 8)}
     return {"seed": 0x5EED0005, "n": n, "len": L, "stride": L,
             "crc_first": [int(x) for x in crc[:8]], "crc_last": int(crc[-1]),
             "digest": p.digest(crc), "sub_digest_blocks": 1_000_000, "sub_digests": [int(x) for x in sub],
-            "ref_checked_blocks": ref_checked,
+            "ranks": ranks, "ref_checked_blocks": ref_checked,
             "how": "oracle restatement (port) over all blocks; reference build (oracle/_ref) on every 10th "
-                   "10^5-block chunk incl. the prefix, identical"}
+                   "10^5-block chunk incl. the prefix, identical; ranks[N].rank_digests = Value() over "
+                   "rank r's CRCs (blocks r, r+N, ...) in local order"}
 
 
 def cfg2_union() -> dict:
@@ -335,7 +340,11 @@ def main() -> None:
         path = os.path.join(GOLDEN, "configs.json")
         with open(path) as f:
             d = json.load(f)
-        d["cfg5"] = cfg5()
+        new = cfg5()
+        if "cfg5" in d:  # regenerated (e.g. to add fields): the pinned values must not move
+            for k in ("digest", "crc_last", "crc_first", "sub_digests"):
+                assert new[k] == d["cfg5"][k], f"cfg5 {k} changed"
+        d["cfg5"] = new
         with open(path, "w") as f:
             json.dump(d, f, indent=1)
         print("cfg5 digest", hex(d["cfg5"]["digest"]), "crc_last", hex(d["cfg5"]["crc_last"]))

@@ -146,6 +146,78 @@ def test_verify_shards_world3(corrupt):
         assert v["digest_ok"] is (not corrupt), (r, v)
 
 
+def _cfg5_worker(rank, world, port, n, entry, result_q):
+    """One rank of bench.py's cfg5 leg on the CPU: rank r's round-robin shard
+    of the config-5 stream (seed 0x5EED0005, global blocks r, r + N, ... as
+    fill_splitmix(first_block=r, block_step=N) lays them out), checksummed
+    by the engine's host path, verified with the leg's own expectations
+    (shard.round_robin_expect over a golden-shaped entry)."""
+    import torch.distributed as dist
+    import oracle
+    from nvlevelz_amd import crc32c, shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p, L = oracle.port(), 4096
+        ids = shard.local_ids(n, rank, world)
+        local = np.array([crc32c.value(p.fill(0x5EED0005, int(i) * L, L)) for i in ids], dtype=np.uint32)
+        v = shard.verify_shards(torch.from_numpy(local.view(np.int32).copy()), n,
+                                shard.round_robin_expect(entry, world))
+        result_q.put((rank, v))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cfg5_leg_partition_and_verify_world2():
+    """bench.py's cfg5 leg at --gpus 2 (strong scaling: the batch's blocks
+    split round-robin, 10^7 on the GPU box; here the first 3001 blocks of the
+    same stream): both ranks' own digests and the gathered digest pass, with
+    the expectations in the golden's shape (cfg5.ranks[N].rank_digests)."""
+    import torch.multiprocessing as mp
+    import oracle
+    p = oracle.port()
+    n, world = 3001, 2
+    whole = p.fixed(p.fill(0x5EED0005, 0, n * 4096), 4096, 4096, n)
+    g = load_golden("configs")["cfg5"]
+    assert whole[:8].tolist() == g["crc_first"]  # the same stream as the golden's
+    entry = {"digest": p.digest(whole), "crc_last": int(whole[-1]),
+             "ranks": {str(world): {"rank_digests": [p.digest(whole[r::world]) for r in range(world)]}}}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cfg5_worker, args=(r, world, port, n, entry, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for r, v in res.items():
+        assert v["rank_digests_ok"] is True and v["digest_ok"] is True and v["crc_last_ok"] is True, (r, v)
+        assert v["blocks_checked"] == n
+
+
+def test_cfg5_golden_rank_expectations():
+    """The cfg5 golden carries per-rank digests for every N the driver runs
+    (bench.py --gpus 1/2/4/8, plus 3); at N = 1 the rank digest is the digest;
+    verify_local reproduces the N = 1 report on a small batch."""
+    from nvlevelz_amd import shard
+    import oracle
+    g = load_golden("configs")["cfg5"]
+    for N in (1, 2, 3, 4, 8):
+        e = shard.round_robin_expect(g, N)
+        assert e["digest"] == g["digest"] and e["crc_last"] == g["crc_last"]
+        assert len(e["rank_digests"]) == N
+    p = oracle.port()
+    whole = p.fixed(p.fill(0x5EED0005, 0, 64 * 4096), 4096, 4096, 64)
+    e = {"digest": p.digest(whole), "crc_last": int(whole[-1]), "rank_digests": [p.digest(whole)]}
+    v = shard.verify_local(whole, e)
+    assert v["digest_ok"] and v["rank_digests_ok"] and v["crc_last_ok"]
+    whole[3] ^= 1
+    assert not shard.verify_local(whole, e)["digest_ok"]
+
+
 def test_partition_math():
     from nvlevelz_amd import shard
     for n in (0, 1, 7, 100000, 10_000_000):

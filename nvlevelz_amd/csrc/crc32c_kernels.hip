@@ -1004,10 +1004,7 @@ __device__ __forceinline__ uint32_t pull_unit(uint8_t* lds, int lane, uint32_t c
 // of a CU finish together (a static per-wave split left the last wave ~20 %
 // behind the mean: older waves win issue arbitration).  U buffers per unit are
 // computed with interleaved chains.
-#ifndef NVL_TAIL
-#define NVL_TAIL 64  // single-buffer units at the end of a range (tools/ab_bench.py: 64 > 32 > 96 > 16 > 0)
-#endif
-constexpr uint32_t kTail = NVL_TAIL;
+constexpr uint32_t kTail = 64;  // single-buffer units at the end of a range (tools/ab_bench.py: 64 > 32 > 96 > 16 > 0)
 
 template <int U, int NW = kWavesPerWG, int M = kAligned, class G = FixedGeom, bool kRaw = false, bool NIB = false>
 __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* lds) {
@@ -3314,15 +3311,9 @@ __device__ __forceinline__ lds_vu32* region_slot(uint8_t* lds, uint32_t r) {
   return (lds_vu32*)(lds + kRNibOff + r * 256u + 252u);
 }
 constexpr uint32_t kSlotOwnLo = 1, kSlotOwnHi = 2, kSlotEndLo = 3, kSlotEndHi = 4, kSlotHalo = 5;
-constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32, 48, 64, 80: T[n][0][63] = 0 in the blob)
-#ifndef NVL_FOLD_SIMD
-#define NVL_FOLD_SIMD 1
-#endif
-// The first search after the LDS fill barrier (which then waits for the fill
-// alone): r 68.75 -> 68.25 us, v 72.58 -> 72.42 us in interleaved A/B.
-#ifndef NVL_SEARCH_LATE
-#define NVL_SEARCH_LATE 1
-#endif
+// (rows 16, 32, 48, 64, 80, 96: T[n][0][63] = 0 in the blob; row 96 counts the
+// workgroup's waves per SIMD, one byte each)
+constexpr uint32_t kSlotReady = 16, kSlotTail = 32, kSlotWaves = 96;
 
 // Scheduler A over the region's chunks, and the per-buffer fold in the same
 // launch.  Workgroup b owns the chunk range [B0, B1) and the buffers
@@ -3341,10 +3332,7 @@ constexpr uint32_t kSlotReady = 16, kSlotTail = 32;  // (rows 16, 32, 48, 64, 80
 // without its records or with chunks outside the workgroup's streamed range
 // is checksummed serially (unsorted or overlapping batches: correct, slow).
 // Buffers must lie inside the region (the entry point's contract).
-#ifndef NVL_RTAIL
-#define NVL_RTAIL 8
-#endif
-constexpr uint32_t kRTail = NVL_RTAIL;  // single-chunk units at the end of a range
+constexpr uint32_t kRTail = 8;  // single-chunk units at the end of a range (64 / 16 / 8 / 0 A/B'd: DESIGN §3.7)
 
 template <int U>
 __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds) {
@@ -3357,26 +3345,35 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint32_t cnt = (uint32_t)(B1 - B0);
   const uint32_t nfull = cnt > kRTail ? (cnt - kRTail) / U : 0u;
   const uint32_t nunits = nfull + (cnt - nfull * U);
-  uint64_t C0 = B0;       // the halo's first chunk (B0: none) -- known once wave 0 published it
-  uint32_t nhalo = ~0u;   // halo units, ~0u until read
-  auto first_of = [&](uint32_t u) -> uint64_t {
-    if (u >= nunits) return C0 + (uint64_t)(u - nunits) * U;
-    return u < nfull ? B0 + (uint64_t)u * U : B0 + (uint64_t)nfull * U + (u - nfull);
-  };
-  auto count_of = [&](uint32_t u) -> uint32_t {
-    if (u >= nunits) {
-      if (nhalo == ~0u) {  // wave 0 publishes right after the LDS fill: long done by now
-        uint32_t r;
-        while ((r = *region_slot(lds, kSlotReady)) == 0u) __builtin_amdgcn_s_sleep(1);
-        nhalo = uniform_u32(r - 1u);
-        const uint64_t h = *region_slot(lds, kSlotHalo);
-        C0 = B0 - uniform_u64(h);
-      }
-      if (u - nunits >= nhalo) return 0u;
-      const uint64_t f = C0 + (uint64_t)(u - nunits) * U;
-      return (uint32_t)min((uint64_t)U, B0 - f);
+  // Unit u's chunks [first, first + count): own units from [B0, B1), halo
+  // units (u >= nunits) from the halo [C0, B0) that wave 0 publishes after
+  // the LDS fill barrier.  One function gives both, and a halo unit's first
+  // chunk is formed only after the published halo has been read: a halo
+  // unit never addresses a chunk from an origin it has not read.  (Round 4
+  // computed them in two lambdas whose halo origin was valid only when the
+  // count was asked first; a variant that called them the other way round
+  // addressed chunks past the region -- DESIGN.md §3.7.)  Every chunk of a
+  // unit lies in [C0, B1) with C0 <= B0 <= B1 <= nc (tests/kernel_model.py
+  // region_schedule asserts it, zero-chunk workgroups and one-buffer
+  // batches included); a unit with count 0 loads nothing.
+  uint64_t C0 = B0;      // the halo's first chunk -- valid once nhalo != ~0u
+  uint32_t nhalo = ~0u;  // halo units, ~0u until read
+  auto span_of = [&](uint32_t u, uint64_t& first) -> uint32_t {
+    if (u < nunits) {
+      first = u < nfull ? B0 + (uint64_t)u * U : B0 + (uint64_t)nfull * U + (u - nfull);
+      return u < nfull ? (uint32_t)U : 1u;
     }
-    return u < nfull ? (uint32_t)U : 1u;
+    if (nhalo == ~0u) {  // wave 0 publishes right after the LDS fill: long done by now
+      uint32_t r;
+      while ((r = *region_slot(lds, kSlotReady)) == 0u) __builtin_amdgcn_s_sleep(1);
+      nhalo = uniform_u32(r - 1u);
+      const uint64_t h = *region_slot(lds, kSlotHalo);
+      C0 = B0 - uniform_u64(h);
+    }
+    first = B0;
+    if (u - nunits >= nhalo) return 0u;
+    first = C0 + (uint64_t)(u - nunits) * U;
+    return (uint32_t)min((uint64_t)U, B0 - first);
   };
   // (Loads behind the branch: the compiler then waits vmcnt(0) at the top
   // of the unit, the next unit's chunks included.  Unconditional loads with
@@ -3403,8 +3400,8 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   // (Two pre-assigned units per wave, 64 MB in flight at the start, delayed
   // the probes' return to ~10 us and lost ~8 us: rejected.)
   uint32_t u = wv;
-  uint64_t ca = first_of(u);
-  uint32_t cu = u < nunits ? count_of(u) : 0u;
+  uint64_t ca = B0;  // (a wave without a pre-assigned unit pulls one after the barrier)
+  uint32_t cu = u < nunits ? span_of(u, ca) : 0u;
   uint32_t un = 0u, cun = 0u;
   uint64_t can = 0u;
   Chunk cur[U], nxt[U];
@@ -3412,21 +3409,19 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const SearchProbe probe = region_probe(g, ca * kChunk, lane);
   asm volatile("" ::: "memory");
   load_unit(ca, cu, cur);
-#if NVL_SEARCH_LATE
+  // The first search after the LDS fill barrier, which then waits for the
+  // fill alone (r 68.75 -> 68.25 us, v 72.58 -> 72.42 us in interleaved A/B).
   fill_region_store(lds, fill, min(nunits, (uint32_t)kWavesPerWG));
   __syncthreads();
   NVL_TL(1);
+  // this wave's SIMD (HW_ID bits 5:4), counted for the fold's slice dealing
+  const uint32_t simd = uniform_u32(__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u);
+  if (lane == 0)
+    __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotWaves)), 1u << (8u * simd), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
   uint64_t cursor = cu ? region_search(g, ca * kChunk, lane, probe) : g.n;
   NVL_TL(6);
   WinRaw wr = load_win(g, cursor, lane);
-#else
-  uint64_t cursor = cu ? region_search(g, ca * kChunk, lane, probe) : g.n;
-  NVL_TL(6);
-  WinRaw wr = load_win(g, cursor, lane);
-  fill_region_store(lds, fill, min(nunits, (uint32_t)kWavesPerWG));
-  __syncthreads();
-  NVL_TL(1);
-#endif
   // wave 0, after the barrier (searches before it held every wave there):
   // the owned buffers [I_b, I_b+1) -- I_b is its own first cursor -- and the
   // halo (the chunks of I_b before B0), published for the halo units and
@@ -3449,8 +3444,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const LaneBase lb = make_lane_base(lane);
   if (!cu) {  // no pre-assigned unit (a range of fewer than 16 units): pull one, maybe a halo unit
     u = pull_unit(lds, lane, kRCtrOff);
-    cu = count_of(u);
-    ca = first_of(u);
+    cu = span_of(u, ca);
     load_unit(ca, cu, cur);
     cursor = cu && u < nunits ? region_search(g, ca * kChunk, lane) : g.n;
     wr = load_win(g, cursor, lane);
@@ -3463,8 +3457,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   // buffers: 8 % slower on v, rejected.)
   while (cu) {
     un = pull_unit(lds, lane, kRCtrOff);
-    cun = count_of(un);  // (first: a halo unit's reads the halo)
-    can = first_of(un);
+    cun = span_of(un, can);
     load_unit(can, cun, nxt);
     const bool halo = u >= nunits;
     const Win w = make_win(g, wr, cursor, lane);
@@ -3549,46 +3542,52 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint64_t ib1 = ((uint64_t)*region_slot(lds, kSlotEndHi) << 32) | *region_slot(lds, kSlotEndLo);
   const uint64_t c0w = B0 - *region_slot(lds, kSlotHalo);  // the first chunk streamed here
   const uint64_t nsl = ib1 > ib ? (ib1 - ib + 63u) / 64u : 0u;
-#if NVL_FOLD_SIMD
-  // slices k = simd (mod 4) to this wave's SIMD (HW_ID bits 5:4): the fold
-  // is VALU-bound, so a SIMD holding two folding waves finishes last.  Every
-  // slice is claimed because every SIMD holds 4 of the 16 waves: at > 64
-  // VGPRs a SIMD takes at most 4 (tests/test_kernel_resources.py pins that;
-  // a fallback to the other SIMDs' counters measured 0.85 us slower on v)
-  const uint32_t simd = uniform_u32(__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u);
+  // slices k = s (mod 4) go to the waves on SIMD s: the fold is VALU-bound,
+  // so a SIMD holding two folding waves finishes last.  A SIMD that holds
+  // none of the workgroup's waves (at <= 64 VGPRs a SIMD may take 5+ of the
+  // 16, or another kernel's waves may fill one) has its slices adopted by
+  // the waves of the lowest populated SIMD once their own run out (the wave
+  // counts are complete at the fold barrier), so every slice is claimed.
+  uint32_t cs = simd;  // the SIMD whose slices this wave claims
   auto claim = [&]() -> uint64_t {
     uint32_t v = 0;
     if (lane == 0)
-      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail + 16u * simd)), 1u,
+      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail + 16u * cs)), 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return (uint64_t)simd + 4u * (uint64_t)uniform_u32(v);
+    return (uint64_t)cs + 4u * (uint64_t)uniform_u32(v);
   };
-#else
-  auto claim = [&]() -> uint64_t {
-    uint32_t v = 0;
-    if (lane == 0)
-      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail)), 1u,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return uniform_u32(v);
-  };
-#endif
   uint64_t k = claim();
   FoldIn f;
   if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
   __syncthreads();
   NVL_TL(3);
   const uint8_t* lsl = lds + (kRSliceOff - kSliceOff);
-  while (k < nsl) {
-    const uint64_t i = ib + 64u * k + (uint64_t)lane;
-    if (i < ib1) {
-      const uint4 q_s = g.qs[i], q_e = g.qe[i];  // (not written for a buffer without that event: unused then)
-      NVL_TL_WAIT(4, q_s.x);
-      uint32_t v = 0u;
-      if (!(f.fast && fold_out(g, lds, lsl, lb, lane, f, q_s, q_e, v)))
-        v = serial_raw(ka.tables + kGSlice, f.ninit, g.grid + f.s, f.L);  // (outside the region too: the caller's memory)
-      NVL_TL_WAIT(5, v);
-      ka.out[i] = finish(~v, ka.flags);
+  uint32_t adopt = 0u;  // empty SIMDs whose slices this wave takes over
+  {
+    const uint32_t wc = *region_slot(lds, kSlotWaves);
+    uint32_t empty = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j) empty |= ((wc >> (8u * j)) & 255u) == 0u ? 1u << j : 0u;
+    adopt = simd == (uint32_t)__builtin_ctz(~empty & 15u) ? uniform_u32(empty) : 0u;
+  }
+  for (;;) {
+    while (k < nsl) {
+      const uint64_t i = ib + 64u * k + (uint64_t)lane;
+      if (i < ib1) {
+        const uint4 q_s = g.qs[i], q_e = g.qe[i];  // (not written for a buffer without that event: unused then)
+        NVL_TL_WAIT(4, q_s.x);
+        uint32_t v = 0u;
+        if (!(f.fast && fold_out(g, lds, lsl, lb, lane, f, q_s, q_e, v)))
+          v = serial_raw(ka.tables + kGSlice, f.ninit, g.grid + f.s, f.L);  // (outside the region too: the caller's memory)
+        NVL_TL_WAIT(5, v);
+        ka.out[i] = finish(~v, ka.flags);
+      }
+      k = claim();
+      if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
     }
+    if (!adopt) break;
+    cs = (uint32_t)__builtin_ctz(adopt);
+    adopt &= adopt - 1u;
     k = claim();
     if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
   }

@@ -570,3 +570,84 @@ def quad_prefix(x: int, quad: bytes, o: int) -> int:
     for b in range(r):
         crc = T[0][(crc ^ (cur >> (8 * b))) & 0xFF] ^ (crc >> 8)
     return crc
+
+
+# ---- region path: the launch's partition (crc32c_kernels.hip run_region) ----
+# Workgroup b of G owns the chunk range [B0, B1) = [nc b / G, nc (b+1) / G)
+# and the buffers [I_b, I_b+1), I_b = the first buffer ending after chunk
+# B0's start (I_0 = 0, I_G = n).  Its units: nfull two-chunk units, then
+# single-chunk tail units, then the halo units re-streaming the chunks
+# [C0, B0) of the one owned buffer that starts before B0.
+
+def region_search(ends, A: int) -> int:
+    """First buffer b with e_b > A (n when none), for non-decreasing ends."""
+    for b, e in enumerate(ends):
+        if e > A:
+            return b
+    return len(ends)
+
+
+def region_units(nc: int, G: int, b: int, U: int = 2, rtail: int = 8):
+    B0, B1 = nc * b // G, nc * (b + 1) // G
+    cnt = B1 - B0
+    nfull = (cnt - rtail) // U if cnt > rtail else 0
+    return B0, B1, nfull, nfull + (cnt - nfull * U)
+
+
+def region_span(u: int, B0: int, nfull: int, nunits: int, C0: int, nhalo: int, U: int = 2):
+    """span_of(u): unit u's chunks (first, count) -- own units from [B0, B1),
+    halo units from [C0, B0) once the halo is known."""
+    if u < nunits:
+        return (B0 + u * U, U) if u < nfull else (B0 + nfull * U + (u - nfull), 1)
+    h = u - nunits
+    if h >= nhalo:
+        return B0, 0
+    f = C0 + h * U
+    return f, min(U, B0 - f)
+
+
+def region_schedule(starts, lens, rel0: int, region_len: int, G: int, U: int = 2, rtail: int = 8, waves: int = 16):
+    """Every workgroup's owned buffers and streamed chunks for a sorted,
+    non-overlapping batch (starts relative to the region), asserting what the
+    kernel relies on: every chunk a unit addresses lies in [0, nc) -- also in
+    workgroups that own no chunk (G > nc) and for one-buffer batches; the
+    owned ranges partition [0, n); every buffer's end lies in its owner's
+    range and each of its chunks is streamed by its owner.  Returns, per
+    workgroup, (owned buffer range, streamed chunk set)."""
+    n = len(starts)
+    nc = (rel0 + region_len + 4095) // 4096
+    s = [rel0 + x for x in starts]
+    ends = [x + L for x, L in zip(s, lens)]
+    out, owned = [], []
+    for b in range(G):
+        B0, B1, nfull, nunits = region_units(nc, G, b, U, rtail)
+        Ib = 0 if b == 0 else region_search(ends, B0 * 4096)
+        Ib1 = n if b == G - 1 else region_search(ends, B1 * 4096)
+        sb = s[Ib] if Ib < n else 0
+        hc = B0 - (sb >> 12) if (Ib < Ib1 and sb < B0 * 4096) else 0
+        nhalo, C0 = (hc + U - 1) // U, B0 - hc
+        streamed = set()
+        for u in range(nunits + nhalo + waves):  # + a count-0 unit per wave: the loop's exit pull
+            f, c = region_span(u, B0, nfull, nunits, C0, nhalo, U)
+            for k in range(c):
+                assert 0 <= f + k < nc and C0 <= f + k < B1, (b, u, f, c, nc)
+                streamed.add(f + k)
+        assert streamed == set(range(C0, B1)), (b, C0, B1)
+        for i in range(Ib, Ib1):
+            if lens[i] >= REGION_DIRECT:
+                assert B0 * 4096 < ends[i] <= B1 * 4096, (b, i)
+                assert all(c in streamed for c in range(s[i] >> 12, (ends[i] - 1 >> 12) + 1)), (b, i)
+        owned.extend(range(Ib, Ib1))
+        out.append(((Ib, Ib1), streamed))
+    assert owned == list(range(n))
+    return out
+
+
+def region_span_stale(u: int, B0: int, nfull: int, nunits: int, nhalo: int, hc: int, U: int = 2):
+    """The round-4 form: first_of(u) with the halo origin C0 still at its
+    initial B0 -- what a halo unit addressed when its first chunk was formed
+    before its count had read the published halo."""
+    if u < nunits:
+        return region_span(u, B0, nfull, nunits, B0, 0, U)
+    h = u - nunits
+    return B0 + h * U, (min(U, hc - h * U) if h < nhalo else 0)

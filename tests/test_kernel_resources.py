@@ -64,12 +64,13 @@ def test_no_vgpr_spills(usage, name):
 
 
 def test_region_fold_claim_placement(usage):
-    """The region fold deals its slices by SIMD (slice k to a wave on SIMD
-    k mod 4, crc32c_kernels.hip run_region): every slice is claimed only if
-    every SIMD holds some of the workgroup's 16 waves, which the register
-    budget guarantees -- above 64 VGPRs a SIMD (512 per lane) takes at most 4
-    waves, so the 16 waves sit 4 per SIMD."""
+    """The region fold deals its slices by SIMD (slice k to the waves on SIMD
+    k mod 4, crc32c_kernels.hip run_region).  Correctness does not depend on
+    where the 16 waves land: a SIMD that holds none of them has its slices
+    adopted by the lowest populated SIMD's waves.  The balance
+    does: above 102 VGPRs (512 per lane and SIMD, granule 8) a SIMD takes at
+    most 4 waves, so the 16 sit 4 per SIMD and every SIMD folds a quarter."""
     hits = [k for k in usage if "crc32c_region_kernel" in k]
     assert hits
     for k in hits:
-        assert usage[k].get("VGPRs", 0) > 64, (k, usage[k])
+        assert usage[k].get("VGPRs", 0) > 102, (k, usage[k])

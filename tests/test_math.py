@@ -233,3 +233,58 @@ def test_region_quad_prefix_from_checkpoints(port):
             c = o >> 4
             x = cps[c - 1] if c else 0
             assert km.quad_prefix(x, piece[16 * c:16 * c + 16], o) == km.raw_bytes(0, piece[:o]), o
+
+
+def _grid_for(nc: int, num_cu: int = 256) -> int:
+    return max(1, min(num_cu, -(-nc // 16)))  # crc32c_kernels.hip grid_for
+
+
+@pytest.mark.parametrize("G", [None, 1, 4, 16, 256])
+@pytest.mark.parametrize("case", ["one_block", "one_block_lead", "one_mib", "one_tiny", "r_shape", "cfg3_like"])
+def test_region_schedule_bounds(case, G):
+    """run_region's partition over the grid (tests/kernel_model.py
+    region_schedule): every chunk address of every unit -- own, tail, halo
+    and the count-0 units the waves pull on their way out -- lies inside the
+    region's chunks, including one-buffer batches (test_gpu_region's n = 1
+    cases) and grids with more workgroups than chunks (workgroups that own
+    no chunk); the owned buffer ranges partition the batch and each buffer's
+    chunks are streamed by its owner.  G None: the launcher's own grid."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    if case == "one_block":
+        starts, lens, rel0 = [0], [4097], 0
+    elif case == "one_block_lead":
+        starts, lens, rel0 = [int(rng.integers(0, 16))], [int(rng.integers(3364, 4110))], 7
+    elif case == "one_mib":
+        starts, lens, rel0 = [5], [1 << 20], 100
+    elif case == "one_tiny":
+        starts, lens, rel0 = [3], [9], 4090
+    elif case == "r_shape":
+        lens = rng.integers(3364, 4110, 3000).tolist()
+        starts = (np.cumsum([0] + [L + 4 for L in lens[:-1]])).tolist()
+        rel0 = 11
+    else:
+        lens = (512 + rng.integers(0, 65025, 400)).tolist()
+        starts = (np.cumsum([0] + lens[:-1])).tolist()
+        rel0 = 0
+    region_len = starts[-1] + lens[-1] + 3
+    nc = (rel0 + region_len + 4095) // 4096
+    km.region_schedule(starts, lens, rel0, region_len, G or _grid_for(nc))
+
+
+def test_region_stale_halo_origin_addresses_past_the_region():
+    """The fault of a round-4 variant: a halo unit whose first
+    chunk was formed from the halo origin's initial value B0 (before the
+    published halo was read) addresses chunks past the region when the halo
+    is longer than the workgroup's own range -- one buffer spanning many
+    workgroups' ranges, owned by the last one.  span_of (the shipped form)
+    reads the halo first (test_region_schedule_bounds)."""
+    starts, lens, rel0 = [5], [1 << 20], 100
+    nc = (rel0 + starts[0] + lens[0] + 4095) // 4096
+    G = 16
+    B0, B1, nfull, nunits = km.region_units(nc, G, G - 1)
+    hc = B0 - ((rel0 + starts[0]) >> 12)
+    nhalo = (hc + 1) // 2
+    addr = [f + k for u in range(nunits, nunits + nhalo)
+            for f, c in [km.region_span_stale(u, B0, nfull, nunits, nhalo, hc)] for k in range(c)]
+    assert max(addr) >= nc  # past the region: the illegal address
+    km.region_schedule(starts, lens, rel0, lens[0] + starts[0], G)  # the shipped span_of stays inside

@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=6.0,
                     help="target seconds per CPU-baseline leg (all-core and 1-thread)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the all-core CPU leg (0 = every physical core this process may run on)")
+                    help="threads of the all-core CPU leg (0 = the physical cores this process may run on, capped by its cgroup CPU quota)")
     ap.add_argument("--cfg5-steps", type=int, default=20,
                     help="timed steps of the BASELINE config-5 leg (10^7 blocks in total, round-robin over the N "
                          "GPUs, strong scaling) reported beside the headline; 0 = skip")
@@ -114,10 +114,21 @@ def cgroup_cpu_max() -> str | None:
     return None
 
 
+def cgroup_cpus() -> int | None:
+    """CPUs the cgroup v2 quota allows this process (ceil(quota / period)), None without a quota."""
+    cm = cgroup_cpu_max()
+    try:
+        q, per = cm.split()
+        return None if q == "max" else max(1, -(-int(q) // int(per)))
+    except (AttributeError, ValueError):
+        return None
+
+
 def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int, reps: int = 5) -> dict:
     """The reference's own util/crc32c.cc + port/port_posix_sse.cc (oracle/_ref;
-    the clean-room port if absent) on this host: every physical core, and one
-    thread.  Each leg is `reps` timed repetitions (median reported, BASELINE.md);
+    the clean-room port if absent) on this host: one thread per physical core
+    the process may use (capped by the cgroup CPU quota; the uncapped
+    all-physical-core figure beside it), and one thread.  Each leg is `reps` timed repetitions (median reported, BASELINE.md);
     one repetition = `passes` passes over each thread's contiguous share of the
     first n blocks inside ONE call (thread start-up paid once), sized from a
     calibration call to ~seconds/reps.  Around every repetition the process's
@@ -150,8 +161,18 @@ def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int, reps: i
         return r, float(np.median(rates)), float(np.median(par)), passes, rates
 
     phys, logical = physical_cores()
-    th = threads if threads > 0 else phys
+    quota = cgroup_cpus()
+    # one thread per CPU the process may actually use: the physical cores of
+    # its affinity set, capped by the cgroup quota (more threads than the
+    # quota only time-slice; that figure is reported beside it)
+    th = threads if threads > 0 else min(phys, quota or phys)
     r_all, gibs_all, par_all, passes_all, rates_all = leg(n, th)
+    over = None
+    if threads <= 0 and phys > th:
+        _, g_o, p_o, pa_o, r_o = leg(n, phys)
+        over = {"value": round(g_o, 3), "unit": "GiB/s", "threads": phys, "effective_parallelism": round(p_o, 2),
+                "repetitions_gibs": [round(x, 2) for x in r_o],
+                "what": "the same leg on one thread per physical core of the affinity set, above the cgroup quota"}
     n1 = min(n, 20000)
     _, gibs_one, par_one, passes_one, rates_one = leg(n1, 1)
     single = None
@@ -186,11 +207,13 @@ def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int, reps: i
         "threads": th, "effective_parallelism": round(par_all, 2),
         "per_thread_gibs": round(gibs_all / max(par_all, 1e-9), 3),
         "sample": f"median of {reps} repetitions x {passes_all} passes over the first {n} x 4 KiB blocks of this "
-                  f"rank's batch ({th} threads = every physical core of the {logical} CPUs in this process's "
-                  f"affinity set, contiguous share per thread; cores = CPU-seconds / wall of the run = "
-                  f"{par_all:.1f}), leveldb::crc32c::Value via port::AcceleratedCRC32C (SSE4.2)",
+                  f"rank's batch ({th} threads = the physical cores of the {logical} CPUs in this process's "
+                  f"affinity set ({phys}) capped by the cgroup quota ({quota} CPUs), contiguous share per thread; "
+                  f"cores = CPU-seconds / wall of the run = {par_all:.1f}), leveldb::crc32c::Value via "
+                  f"port::AcceleratedCRC32C (SSE4.2)",
         "repetitions_gibs": [round(x, 2) for x in rates_all],
-        "cgroup_cpu_max": cgroup_cpu_max(),
+        "cgroup_cpu_max": cgroup_cpu_max(), "cgroup_cpus": quota,
+        "threads_over_quota": over,
         "single_thread": {"value": round(gibs_one, 3), "unit": "GiB/s", "cores": 1,
                           "effective_parallelism": round(par_one, 2),
                           "sample": f"median of {reps} x {passes_one} passes over {n1} blocks",

@@ -177,18 +177,18 @@ NVL_API int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengt
                           const uint32_t* init, uint32_t init_all, uint32_t* out,
                           uint64_t n, uint32_t flags);
 
-/* Host fixed-stride batch (one contiguous host region, e.g. an mmap'd table
- * file or a pinned bench buffer), pipelined H2D/compute/D2H over two
- * streams.  Synchronous. */
 /* Host region variant: n buffers that all lie inside ONE host region
  * [region, region + region_len) (a file image, a log block run): buffer i is
- * region[offsets[i] .. offsets[i]+lengths[i]).  The region is staged once
- * (one pinned copy, one H2D), then batched as nvl_crc32c_batch_dev.
+ * region[offsets[i] .. offsets[i]+lengths[i]).  The covered range is staged
+ * once (one pinned copy, one H2D), then batched as nvl_crc32c_batch_dev.
  * Synchronous. */
 NVL_API int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const uint64_t* offsets,
                                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all,
                                          uint32_t* out, uint64_t n, uint32_t flags);
 
+/* Host fixed-stride batch (one contiguous host region, e.g. an mmap'd table
+ * file or a pinned bench buffer), pipelined H2D/compute/D2H over two
+ * streams.  Synchronous. */
 NVL_API int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint64_t n,
                           const uint32_t* init, uint32_t init_all, uint32_t* out,
                           uint32_t flags);

@@ -216,7 +216,15 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   const uint64_t nf = nm_max;
   uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
   uint8_t* mv = pin + p_slots + nf * 16;
-  uint64_t prev_end = 0;
+  // (a leading slot that is not read sits at the first read meta block's
+  // offset, else at the index block's: never before the data blocks)
+  uint64_t prev_end = index_h.offset;
+  for (uint64_t j = 0; j < nm; ++j) {
+    if (!meta_bad[j] && block_in_file(meta_blocks[j], len)) {
+      prev_end = meta_blocks[j].offset;
+      break;
+    }
+  }
   for (uint64_t j = 0; j < nf; ++j) {
     if (j < nm) {
       const nvl_block_handle& b = meta_blocks[j];

@@ -33,6 +33,7 @@
 // with ONE v_perm_b32 per lookup from the data word and a per-lane base.
 #include <hip/hip_ext.h>
 #include <atomic>
+#include <random>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -2897,9 +2898,9 @@ struct RegionGeom {
   const uint32_t* init;  // per-buffer Extend seeds (nullptr: init_all)
   uint32_t init_all;
   uint32_t* raws;  // [nc]
-  uint4* qs;       // [n] buffer i's start event: {Qe, lane L's chain checkpoint x_4c, gen, 0}
+  uint4* qs;       // [n] buffer i's start event: {Qe, lane L's chain checkpoint x_4c, gen, i}
   uint4* qe;       // [n] its end event
-  uint32_t gen;    // this call's generation: a record without it was not written by this call
+  uint32_t gen;    // this call's generation: a record without it (and its own index) was not written by this call
 };
 
 typedef const __attribute__((address_space(1))) uint64_t* g64_ptr;
@@ -3084,8 +3085,8 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, Win w, uint64
   for (;;) {
     uint2 rs, re;
     const bool fs = le.sv && rec(le.ps, rs), fe = le.ev && rec(le.pe, re);
-    if (fs) g.qs[cur + (uint64_t)lane] = make_uint4(rs.x, rs.y, g.gen, 0u);
-    if (fe) g.qe[cur + (uint64_t)lane] = make_uint4(re.x, re.y, g.gen, 0u);
+    if (fs) g.qs[cur + (uint64_t)lane] = make_uint4(rs.x, rs.y, g.gen, (uint32_t)(cur + (uint64_t)lane));
+    if (fe) g.qe[cur + (uint64_t)lane] = make_uint4(re.x, re.y, g.gen, (uint32_t)(cur + (uint64_t)lane));
     const uint64_t ms = __ballot(le.sv && !fs), me = __ballot(le.ev && !fe);
     uint64_t all = ms | me;
     while (all) {  // events on another lane than their chunk's first
@@ -3103,7 +3104,7 @@ __device__ __forceinline__ void region_events(const RegionGeom& g, Win w, uint64
 #pragma unroll
           for (int m = 0; m < 3; ++m) x = (k == (uint32_t)q && c == (uint32_t)m + 1u) ? cp[q][m] : x;
         }
-        const uint4 r = make_uint4(lane_u32(v, L), lane_u32(x, L), g.gen, 0u);
+        const uint4 r = make_uint4(lane_u32(v, L), lane_u32(x, L), g.gen, (uint32_t)(cur + j));
         if (lane == 0) (t ? g.qe : g.qs)[cur + j] = r;
       }
     }
@@ -3266,12 +3267,12 @@ __device__ __forceinline__ uint32_t sh4096_lds(const uint8_t* lds, uint32_t acc,
 
 __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds, const uint8_t* lsl,
                                          const LaneBase& lb, int lane, const FoldIn& f, const uint4& q_s,
-                                         const uint4& q_e, uint32_t& v) {
+                                         const uint4& q_e, uint32_t ti, uint32_t& v) {
   const uint64_t s = f.s, e = f.s + f.L;
   const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
   const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
   const uint32_t r0 = g.raws[c0], r1 = g.raws[c1], rm = g.raws[min(c0 + 1u, c1)];
-  if ((os && q_s.z != g.gen) || (oe != kChunk && q_e.z != g.gen)) return false;
+  if ((os && (q_s.z != g.gen || q_s.w != ti)) || (oe != kChunk && (q_e.z != g.gen || q_e.w != ti))) return false;
   const uint32_t qs = os ? q_s.x : 0u;                                   // chunk c0's bytes before s, at its end
   const uint32_t T = (os ? quad_prefix_lds(lsl, lb, q_s.y, f.vs, s & 63u) : 0u) ^ f.ninit;  // R(s) ^ ~init, at s
   const uint32_t ze = oe == kChunk ? r1 : q_e.x;                         // chunk c1's bytes before e, at its end
@@ -3511,7 +3512,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         if (os) {
           const uint32_t L = os >> 6, c = (os >> 4) & 3u;
           const uint32_t x = c == 1u ? cp[0][0] : (c == 2u ? cp[0][1] : cp[0][2]);
-          const uint4 r = make_uint4(lane_u32(pre[0], L), c ? lane_u32(x, L) : 0u, g.gen, 0u);
+          const uint4 r = make_uint4(lane_u32(pre[0], L), c ? lane_u32(x, L) : 0u, g.gen, (uint32_t)ib);
           if (lane == 0) g.qs[ib] = r;
         }
       }
@@ -3577,7 +3578,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         const uint4 q_s = g.qs[i], q_e = g.qe[i];  // (not written for a buffer without that event: unused then)
         NVL_TL_WAIT(4, q_s.x);
         uint32_t v = 0u;
-        if (!(f.fast && fold_out(g, lds, lsl, lb, lane, f, q_s, q_e, v)))
+        if (!(f.fast && fold_out(g, lds, lsl, lb, lane, f, q_s, q_e, (uint32_t)i, v)))
           v = serial_raw(ka.tables + kGSlice, f.ninit, g.grid + f.s, f.L);  // (outside the region too: the caller's memory)
         NVL_TL_WAIT(5, v);
         ka.out[i] = finish(~v, ka.flags);
@@ -3930,9 +3931,11 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
   uint32_t* raws = reinterpret_cast<uint32_t*>(w);
   uint4* qs = reinterpret_cast<uint4*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
   uint4* qe = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 16u));
-  // A process-wide call generation (never 0, the zeroed workspace's value):
-  // the fold trusts an event record only when it carries this call's.
-  static std::atomic<uint32_t> s_gen{0};
+  // A process-wide call generation (never 0, the zeroed workspace's value),
+  // seeded at random so that leftover memory is unlikely to hold it: the
+  // fold trusts an event record only when it carries this call's generation
+  // AND its own buffer index (workspace memory is never zeroed).
+  static std::atomic<uint32_t> s_gen{(uint32_t)std::random_device{}()};
   uint32_t gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
   if (gen == 0u) gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
   dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, init, init_all,

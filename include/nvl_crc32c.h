@@ -64,6 +64,15 @@ extern "C" {
                                       i.e. the on-disk trailer/header value of
                                       table/table_builder.cc:187 and
                                       db/log_writer.cc:96 */
+#define NVL_CRC32C_FLAG_REGION_SHAPED 0x2u  /* nvl_crc32c_region_dev only: the caller has checked
+                                              that the batch is region-shaped (see there), so the
+                                              call is the region kernel alone, one launch.  A
+                                              batch that is not still gets correct results, by
+                                              a slow per-buffer path. */
+
+/* Longest buffer the region path takes: a batch holding a longer one runs
+ * the batch path (it would be re-streamed and folded serially). */
+#define NVL_CRC32C_REGION_MAX_LEN (128u << 10)
 
 /* ---- lifecycle ---------------------------------------------------------- */
 
@@ -133,7 +142,12 @@ NVL_API size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, u
  * addresses in `offsets`).  Arbitrary alignment and length (0 included).
  * out[i] = Extend(init_i, buffer i) (Mask()ed with NVL_CRC32C_FLAG_MASK).
  * Replaces per-call Value/Extend at table/format.cc:90-92 (block verify),
- * db/log_reader.cc:255-256 and db/log_writer.cc:95 (records). */
+ * db/log_reader.cc:255-256 and db/log_writer.cc:95 (records).
+ * The layout is checked on the device (a plan kernel over the metadata): a
+ * region-shaped batch -- sorted by offset, non-overlapping, every buffer at
+ * most NVL_CRC32C_REGION_MAX_LEN bytes, gaps between buffers at most 1/8 of
+ * the buffer bytes + 64 KiB -- is checksummed over its own span by the
+ * region path (see nvl_crc32c_region_dev), any other by the batch kernels. */
 NVL_API int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64_t* lengths,
                          const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* workspace, size_t workspace_bytes,
@@ -149,10 +163,12 @@ NVL_API size_t nvl_crc32c_batch_workspace_bytes(uint64_t n);
  * a log image's records, a packed batch.  The region is checksummed in its
  * own page-aligned 4 KiB chunks at the fixed-stride path's rate whatever the
  * buffers' lengths and alignment, and each out[i] is derived from the chunk
- * values (Mask()ed with NVL_CRC32C_FLAG_MASK).  A batch that breaks the
- * layout (unsorted, overlapping, outside the region) still gets correct
- * results, by a slow serial path: use nvl_crc32c_batch_dev for such batches.
- * Gaps between buffers cost their bytes (the whole region is read). */
+ * values (Mask()ed with NVL_CRC32C_FLAG_MASK).  Gaps between buffers cost
+ * their bytes (the whole region is read).  The layout is checked on the
+ * device first: a batch that is not region-shaped (unsorted, overlapping, a
+ * buffer outside the region or longer than NVL_CRC32C_REGION_MAX_LEN) runs
+ * the batch kernels of nvl_crc32c_batch_dev.  NVL_CRC32C_FLAG_REGION_SHAPED
+ * skips the check (one launch instead of three). */
 NVL_API int nvl_crc32c_region_dev(const void* region, uint64_t region_len, const uint64_t* offsets,
                                   const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
                                   uint64_t n, uint32_t flags, void* workspace, size_t workspace_bytes, void* stream);
@@ -164,7 +180,8 @@ NVL_API int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len,
                                         uint32_t* out, uint64_t n, uint32_t flags, void* workspace,
                                         size_t workspace_bytes, void* stream, void* start_event, void* stop_event);
 
-/* Workspace bytes nvl_crc32c_region_dev needs (4 B per 4 KiB of region + 32 B per buffer). */
+/* Workspace bytes nvl_crc32c_region_dev needs (4 B per 4 KiB of region + 32 B
+ * per buffer for the region path, plus the batch path's workspace). */
 NVL_API size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n);
 
 /* ---- batched, host-resident (end-to-end path) ---------------------------- */

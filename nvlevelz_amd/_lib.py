@@ -25,6 +25,8 @@ ENODEV = -3
 ESELFTEST = -4
 ENOSPC = -5
 FLAG_MASK = 0x1
+FLAG_REGION_SHAPED = 0x2  # nvl_crc32c_region_dev: the caller checked the layout (one launch)
+REGION_MAX_LEN = 128 << 10
 
 _c = ctypes
 _vp = _c.c_void_p

@@ -248,12 +248,16 @@ def region_workspace_bytes(region_len: int, n: int) -> int:
     return int(lib.nvl_crc32c_region_workspace_bytes(region_len, n))
 
 
-def extend_region(buf, offsets, lengths, init=0, *, mask: bool = False, out=None, workspace=None):
+def extend_region(buf, offsets, lengths, init=0, *, mask: bool = False, out=None, workspace=None,
+                  shaped: bool = False):
     """out[i] = Extend(init_i, buf[offsets[i] : offsets[i] + lengths[i]]) for
     buffers inside ``buf`` sorted by offset and non-overlapping (an SSTable
     image's blocks, a packed batch): nvl_crc32c_region_dev, which reads the
-    whole of ``buf`` in page-aligned 4 KiB chunks.  Other layouts are correct
-    but slow there; use extend_batch for them.  Asynchronous."""
+    whole of ``buf`` in page-aligned 4 KiB chunks.  The layout is checked on
+    the device (other layouts run the batch kernels); ``shaped=True``
+    (NVL_CRC32C_FLAG_REGION_SHAPED) skips the check for a caller that has made
+    it itself -- one launch, and a slow per-buffer path if it was wrong.
+    Asynchronous."""
     torch = _torch()
     _require_dev(buf, "buf", (torch.uint8, torch.int8))
     _require_dev(offsets, "offsets", (torch.int64, torch.uint64), buf.device)
@@ -278,9 +282,9 @@ def extend_region(buf, offsets, lengths, init=0, *, mask: bool = False, out=None
     if workspace is not None:
         _require_dev(workspace, "workspace", None, buf.device)
         ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    flags = (FLAG_MASK if mask else 0) | (_lib.FLAG_REGION_SHAPED if shaped else 0)
     rc = lib.nvl_crc32c_region_dev(buf.data_ptr(), buf.numel(), offsets.data_ptr(), lengths.data_ptr(), init_ptr,
-                                   init_all, out.data_ptr(), n, FLAG_MASK if mask else 0, ws_ptr, ws_bytes,
-                                   _stream_handle(buf))
+                                   init_all, out.data_ptr(), n, flags, ws_ptr, ws_bytes, _stream_handle(buf))
     check(rc, "nvl_crc32c_region_dev")
     return out
 
@@ -347,5 +351,5 @@ def to_u32(t) -> np.ndarray:
 
 
 __all__ = ["extend", "value", "mask", "unmask", "kMaskDelta", "init", "gpu_accelerated",
-           "extend_fixed", "FixedBatch", "extend_batch", "extend_batch_host", "extend_fixed_host",
+           "extend_fixed", "FixedBatch", "extend_batch", "extend_region", "extend_batch_host", "extend_fixed_host",
            "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix", "to_u32", "Crc32cError"]

@@ -21,6 +21,8 @@
 
 namespace nvl {
 
+static_assert(kRegionMaxLen == NVL_CRC32C_REGION_MAX_LEN, "the route's length limit is the header's");
+
 void build_device_tables(uint32_t* w) {
   uint32_t slice[4][256];
   build_slice4(slice);
@@ -192,24 +194,28 @@ DeviceState* current_state(int* rc) {
   return state_for(dev, rc);
 }
 
-// Variable-batch workspace: [counts n+1][chunk_start n+1][unit map][records][head contributions n][scan scratch]
-// [chunk counts][chunk_start][unit map][records][hc][flags: long_bufs][scan temp]
-size_t batch_ws_layout(uint64_t n, int num_cu, size_t* off_cs, size_t* off_map, size_t* off_recs, size_t* off_hc,
-                       size_t* off_flags, size_t* off_tmp) {
+// Variable-batch workspace: [chunk counts n+1][chunk_start n+1 (fused: lpre)]
+// [unit map (fused: tiles)][records][hc: n u32][flags: long_bufs][scan temp]
+// then, for a routed call, [route partials][region workspace: `cap` chunk raws
+// + 2 x n event records].
+struct BatchWs {
+  size_t cs, map, recs, hc, flags, tmp, parts, region, total;
+  uint64_t cap;  // region chunk raws (0: no routed part)
+};
+BatchWs batch_ws(uint64_t n, int num_cu, uint64_t cap) {
+  BatchWs w;
   const size_t cnt = align_up((n + 1) * sizeof(uint64_t), 256);
-  const size_t cs = cnt;
-  const size_t map = align_up(var_unit_map_bytes(num_cu), 256);
-  const size_t recs = align_up(var_recs_bytes(num_cu), 256);
-  const size_t hc = align_up(n * sizeof(uint32_t), 256);
-  const size_t fl = 256;
-  const size_t tmp = align_up(scan_temp_bytes(n + 1), 256);
-  *off_cs = cnt;
-  *off_map = cnt + cs;
-  *off_recs = cnt + cs + map;
-  *off_hc = cnt + cs + map + recs;
-  *off_flags = cnt + cs + map + recs + hc;
-  *off_tmp = cnt + cs + map + recs + hc + fl;
-  return cnt + cs + map + recs + hc + fl + tmp;
+  w.cs = cnt;
+  w.map = w.cs + cnt;
+  w.recs = w.map + align_up(var_unit_map_bytes(num_cu), 256);
+  w.hc = w.recs + align_up(var_recs_bytes(num_cu), 256);
+  w.flags = w.hc + align_up(n * sizeof(uint32_t), 256);
+  w.tmp = w.flags + 256;
+  w.parts = w.tmp + align_up(scan_temp_bytes(n + 1), 256);
+  w.region = w.parts + (cap ? route_parts_bytes() : 0);
+  w.total = w.region + (cap ? region_ws_bytes_cap(cap, n) : 0);
+  w.cap = cap;
+  return w;
 }
 
 size_t fixed_ws_bytes(uint64_t len, uint64_t n, int num_cu) { return fixed_recs_bytes(num_cu, len, n); }
@@ -237,36 +243,42 @@ int do_fixed(DeviceState* s, const void* base, uint64_t stride, uint64_t len, ui
   return hip_rc(e);
 }
 
+// A variable-length batch.  routed: the device decides (launch_routed: the
+// region path for a region-shaped batch, else the head + body kernels) --
+// for metadata only the device holds (nvl_crc32c_batch_dev); otherwise the
+// head + body kernels, max_len a host-known bound on the lengths.
 int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const uint64_t* lengths,
              const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags, void* ws,
-             size_t ws_bytes, hipStream_t st, uint64_t max_len = UINT64_MAX) {
+             size_t ws_bytes, hipStream_t st, uint64_t max_len = UINT64_MAX, bool routed = false) {
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out) return NVL_CRC32C_EINVAL;
   if (n >= (1ull << 31) - 2) return NVL_CRC32C_EINVAL;
-  size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
-  const size_t need = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
+  const BatchWs L = batch_ws(n, s->num_cu, routed ? route_cap_chunks(n) : 0);
   bool own = false;
   if (!ws) {
-    if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
+    if (hipMallocAsync(&ws, L.total, st) != hipSuccess) return NVL_CRC32C_EHIP;
     own = true;
-  } else if (ws_bytes < need) {
+  } else if (ws_bytes < L.total) {
     return NVL_CRC32C_ENOSPC;
   }
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint64_t* cnt = reinterpret_cast<uint64_t*>(w);
-  uint64_t* cs = reinterpret_cast<uint64_t*>(w + off_cs);
-  uint64_t* unit_first = reinterpret_cast<uint64_t*>(w + off_map);
-  Rec* recs = reinterpret_cast<Rec*>(w + off_recs);
-  uint32_t* hc = reinterpret_cast<uint32_t*>(w + off_hc);
-  uint32_t* long_bufs = reinterpret_cast<uint32_t*>(w + off_flags);
-  void* tmp = w + off_tmp;
+  uint64_t* cs = reinterpret_cast<uint64_t*>(w + L.cs);
+  uint64_t* unit_first = reinterpret_cast<uint64_t*>(w + L.map);
+  Rec* recs = reinterpret_cast<Rec*>(w + L.recs);
+  uint32_t* hc = reinterpret_cast<uint32_t*>(w + L.hc);
+  uint32_t* long_bufs = reinterpret_cast<uint32_t*>(w + L.flags);
+  void* tmp = w + L.tmp;
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   const bool small = var_plan_small(n);
 #if !defined(NVL_NO_FUSED)
   if (s->num_cu <= 1023) lc.counter = counters_for(s, st);
   if (lc.counter) {  // (cs holds lpre, the unit map region the tiles)
-    hipError_t ef = launch_var_fused(lc, static_cast<const uint8_t*>(base), offsets, lengths, n, init, init_all, out,
-                                     flags, recs, hc, cs, unit_first, max_len);
+    hipError_t ef =
+        routed ? launch_routed(lc, static_cast<const uint8_t*>(base), 0, true, offsets, lengths, n, init, init_all, out,
+                               flags, w + L.region, L.cap, w + L.parts, recs, hc, cs, unit_first)
+               : launch_var_fused(lc, static_cast<const uint8_t*>(base), offsets, lengths, n, init, init_all, out,
+                                  flags, recs, hc, cs, unit_first, max_len);
     if (own) (void)hipFreeAsync(ws, st);
     return hip_rc(ef);
   }
@@ -276,7 +288,7 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
     e = launch_var_plan_small(lc, lengths, n, cs, unit_first, long_bufs);
   } else {
     e = launch_var_counts(lengths, n, cnt, long_bufs, st);
-    if (e == hipSuccess) e = exclusive_scan_u64(tmp, need - off_tmp, cnt, cs, n + 1, st);
+    if (e == hipSuccess) e = exclusive_scan_u64(tmp, L.parts - L.tmp, cnt, cs, n + 1, st);
   }
   if (e == hipSuccess)
     e = launch_var(lc, static_cast<const uint8_t*>(base), offsets, lengths, cs, unit_first, n, init, init_all, out,
@@ -285,16 +297,29 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   return hip_rc(e);
 }
 
-// Region batch: page-aligned chunk pass + per-buffer fold (launch_region).
+// Workspace of a checked region call: the routed batch workspace with the
+// caller's region as the region part.
+size_t region_checked_ws_bytes(uint64_t region_len, uint64_t n, int num_cu) {
+  return batch_ws(n, num_cu, region_cap_chunks(region_len)).total;
+}
+
+// Region batch.  checked (nvl_crc32c_region_dev: the layout is the device's
+// to check): routed over the caller's region -- a batch that is not
+// region-shaped (unsorted, overlapping, outside the region, a buffer longer
+// than kRegionMaxLen) runs the batch path.  Unchecked (the host has checked
+// the layout itself): the region kernel alone, one launch.
 int do_region(DeviceState* s, const void* region, uint64_t region_len, const uint64_t* offsets,
               const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
               uint32_t flags, void* ws, size_t ws_bytes, hipStream_t st, hipEvent_t ev_start = nullptr,
-              hipEvent_t ev_stop = nullptr) {
+              hipEvent_t ev_stop = nullptr, bool checked = true) {
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out || !region) return NVL_CRC32C_EINVAL;
   if (n >= (1ull << 31) - 2 || region_len > (1ull << 50)) return NVL_CRC32C_EINVAL;
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr, ev_start, ev_stop};
-  const size_t need = region_ws_bytes(region_len, n);
+  if (checked && s->num_cu <= 1023) lc.counter = counters_for(s, st);
+  checked = checked && lc.counter;
+  const BatchWs L = batch_ws(n, s->num_cu, region_cap_chunks(region_len));
+  const size_t need = checked ? L.total : region_ws_bytes(region_len, n);
   bool own = false;
   if (!ws) {
     if (hipMallocAsync(&ws, need, st) != hipSuccess) return NVL_CRC32C_EHIP;
@@ -302,8 +327,14 @@ int do_region(DeviceState* s, const void* region, uint64_t region_len, const uin
   } else if (ws_bytes < need) {
     return NVL_CRC32C_ENOSPC;
   }
-  hipError_t e = launch_region(lc, static_cast<const uint8_t*>(region), region_len, offsets, lengths, init, init_all,
-                               out, n, flags, ws);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  hipError_t e =
+      checked ? launch_routed(lc, static_cast<const uint8_t*>(region), region_len, false, offsets, lengths, n, init,
+                              init_all, out, flags, w + L.region, L.cap, w + L.parts, reinterpret_cast<Rec*>(w + L.recs),
+                              reinterpret_cast<uint32_t*>(w + L.hc), reinterpret_cast<uint64_t*>(w + L.cs),
+                              reinterpret_cast<uint64_t*>(w + L.map))
+              : launch_region(lc, static_cast<const uint8_t*>(region), region_len, offsets, lengths, init, init_all,
+                              out, n, flags, ws);
   if (own) (void)hipFreeAsync(ws, st);
   return hip_rc(e);
 }
@@ -666,9 +697,7 @@ size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, uint64_t 
 size_t nvl_crc32c_batch_workspace_bytes(uint64_t n) {
   int rc = NVL_CRC32C_OK;
   DeviceState* s = current_state(&rc);
-  size_t a, b, c, d, e;
-  size_t f;
-  return batch_ws_layout(n, s ? s->num_cu : 256, &a, &b, &c, &d, &f, &e);
+  return batch_ws(n, s ? s->num_cu : 256, route_cap_chunks(n)).total;
 }
 
 int nvl_crc32c_fixed_dev(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
@@ -705,10 +734,14 @@ int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64
   DeviceState* s = state_for(dev, &rc);
   if (!s) return rc;
   return do_batch(s, base, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
-                  static_cast<hipStream_t>(stream));
+                  static_cast<hipStream_t>(stream), UINT64_MAX, /*routed=*/true);
 }
 
-size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n) { return region_ws_bytes(region_len, n); }
+size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n) {
+  int rc = NVL_CRC32C_OK;
+  DeviceState* s = current_state(&rc);
+  return region_checked_ws_bytes(region_len, n, s ? s->num_cu : 256);
+}
 
 int nvl_crc32c_region_dev(const void* region, uint64_t region_len, const uint64_t* offsets, const uint64_t* lengths,
                           const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags,
@@ -718,8 +751,9 @@ int nvl_crc32c_region_dev(const void* region, uint64_t region_len, const uint64_
   if (rc != NVL_CRC32C_OK) return rc;
   DeviceState* s = state_for(dev, &rc);
   if (!s) return rc;
-  return do_region(s, region, region_len, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
-                   static_cast<hipStream_t>(stream));
+  return do_region(s, region, region_len, offsets, lengths, init, init_all, out, n, flags & NVL_CRC32C_FLAG_MASK,
+                   workspace, workspace_bytes, static_cast<hipStream_t>(stream), nullptr, nullptr,
+                   !(flags & NVL_CRC32C_FLAG_REGION_SHAPED));
 }
 
 int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len, const uint64_t* offsets,
@@ -731,9 +765,9 @@ int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len, const u
   if (rc != NVL_CRC32C_OK) return rc;
   DeviceState* s = state_for(dev, &rc);
   if (!s) return rc;
-  return do_region(s, region, region_len, offsets, lengths, init, init_all, out, n, flags, workspace, workspace_bytes,
-                   static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
-                   static_cast<hipEvent_t>(stop_event));
+  return do_region(s, region, region_len, offsets, lengths, init, init_all, out, n, flags & NVL_CRC32C_FLAG_MASK,
+                   workspace, workspace_bytes, static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
+                   static_cast<hipEvent_t>(stop_event), !(flags & NVL_CRC32C_FLAG_REGION_SHAPED));
 }
 
 int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, const uint32_t* init,
@@ -768,8 +802,7 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
   hipStream_t st = thread_stream(s->device);
   if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
-  size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
-  const size_t ws = batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
+  const size_t ws = batch_ws(n, s->num_cu, 0).total;
   const size_t dbytes = total + n * 4 + ws + 512;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
@@ -843,10 +876,10 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   hipStream_t st = thread_stream(s->device);
   if (!st) return NVL_CRC32C_EHIP;
   uint8_t* d = nullptr;
-  size_t off_cs, off_map, off_recs, off_hc, off_flags, off_tmp;
-  const bool sorted = region_sorted(offsets, lengths, n);
-  const size_t ws = sorted ? region_ws_bytes(wbytes, n)
-                           : batch_ws_layout(n, s->num_cu, &off_cs, &off_map, &off_recs, &off_hc, &off_flags, &off_tmp);
+  // region-shaped (checked here, on the host): the region kernel alone;
+  // otherwise the batch path with the host's bound on the lengths
+  const bool as_region = max_len <= kRegionMaxLen && region_sorted(offsets, lengths, n);
+  const size_t ws = as_region ? region_ws_bytes(wbytes, n) : batch_ws(n, s->num_cu, 0).total;
   const size_t dbytes = align_up(total, 256) + align_up(n * 4, 256) + ws + 256;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
   uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
@@ -864,9 +897,10 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     hini[i] = init ? init[i] : init_all;
   }
   if (e == hipSuccess) e = hipMemcpyAsync(d + meta_off, hst + meta_off, total - meta_off, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && sorted)
+  if (e == hipSuccess && as_region)
     rc = do_region(s, d, wbytes, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
-                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st);
+                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, nullptr, nullptr,
+                   /*checked=*/false);
   else if (e == hipSuccess)
     rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, max_len);

@@ -98,6 +98,25 @@ bool var_heads_only(int num_cu, uint64_t n, uint64_t max_len);
 // folded per buffer in the same launch.  ws: region_ws_bytes(region_len, n)
 // (chunk raws and gen-tagged event records; never needs resetting).
 size_t region_ws_bytes(uint64_t region_len, uint64_t n);
+uint64_t region_cap_chunks(uint64_t region_len);                  // raws the region workspace holds
+size_t region_ws_bytes_cap(uint64_t cap_chunks, uint64_t n);      // a region workspace for cap_chunks raws
+
+// Routed batch over device metadata (nvl_crc32c_batch_dev: dyn, the region
+// is the batch's own span; nvl_crc32c_region_dev: the caller's region):
+// crc32c_route_plan -> crc32c_route_kernel (region path or heads) ->
+// crc32c_var_fused_kernel (returns at once on the region path).  Needs the
+// stream's counter block (lc.counter), the launch_var_fused workspace (recs,
+// hc, lpre, tiles), route_parts_bytes() of plan partials and a region
+// workspace of region_ws_bytes_cap(cap_chunks, n) (dyn: cap_chunks =
+// route_cap_chunks(n); region_dev: region_cap_chunks(region_len)).
+size_t route_parts_bytes();
+uint64_t route_cap_chunks(uint64_t n);
+hipError_t launch_routed(const LaunchCtx& lc, const uint8_t* base, uint64_t region_len, bool dyn,
+                         const uint64_t* offsets, const uint64_t* lengths, uint64_t n, const uint32_t* init,
+                         uint32_t init_all, uint32_t* out, uint32_t flags, void* region_ws, uint64_t cap_chunks,
+                         void* parts_ws, Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles);
+// The longest buffer the region path takes (a longer one: the batch path).
+constexpr uint64_t kRegionMaxLen = 128ull << 10;
 hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* ws);

@@ -291,6 +291,29 @@ __device__ __forceinline__ T ldc(const T* p, uint64_t i) {
   return ((const __attribute__((address_space(4))) T*)p)[i];
 }
 
+// Route plan of a batch over device metadata (nvl_crc32c_batch_dev,
+// nvl_crc32c_region_dev): crc32c_route_plan checks the offsets and lengths
+// in slices and writes one partial per slice; every later launch of the
+// call reduces the same partials (route_region: one wave-wide load, a ballot
+// and a sum) and takes the same decision -- the region path for a
+// region-shaped batch, the head + body kernels otherwise.  No atomics, no
+// reset: the partials are plain stores of the plan launch.
+struct RoutePart {
+  uint64_t sum;  // sum of the slice's lengths, each capped at kRegionMaxLen + 1 (< 2^43 for n < 2^31)
+  uint64_t bad;  // 1: a pair out of order / overlapping, a buffer outside the region or longer than kRegionMaxLen
+};
+constexpr uint32_t kRoutePlanMax = 64;  // plan workgroups (one wave reduces their partials)
+struct Route {
+  const RoutePart* parts = nullptr;  // nullptr: no route (the launch is what it is)
+  uint32_t np = 0;
+  uint32_t dyn = 0;                  // 1: geometry from the batch (batch_dev), gap rule; 0: the caller's region
+  const uint8_t* base = nullptr;     // dyn: the offsets' base (nullptr: absolute addresses)
+  const uint64_t* offsets = nullptr; // the batch's metadata (dyn: its span from the first and last buffer)
+  const uint64_t* lengths = nullptr;
+  uint64_t n = 0;
+  uint64_t cap_chunks = 0;           // dyn: region chunks the workspace holds
+};
+
 struct KArgs {
   uint32_t* out;
   uint32_t flags;
@@ -321,7 +344,50 @@ struct KArgs {
   // Chunk-parallel aligned batches (crc32c_chunks_kernel): the raw register
   // of every 4 KiB chunk, folded per buffer by crc32c_fold_kernel.
   uint32_t* raws = nullptr;
+  // Routed batches (crc32c_route_kernel, crc32c_var_fused_kernel): the plan.
+  Route route{};
 };
+
+// Inclusive sum over the wave by DPP (row_shr 1/2/4/8, row_bcast 15/31): lane 63 holds the total.
+__device__ __forceinline__ uint32_t add_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+  return x;
+}
+
+// The wave's total of a u64 whose per-lane values are < 2^43, in two DPP sums
+// (bits 20.. and 0..19: each total fits 32 bits).
+__device__ __forceinline__ uint64_t wave_total_u64(uint64_t v) {
+  const uint32_t h = add_scan((uint32_t)(v >> 20)), l = add_scan((uint32_t)v & 0xFFFFFu);
+  return ((uint64_t)lane_u32(h, 63u) << 20) + lane_u32(l, 63u);
+}
+
+
+// The verdict, as every launch after the plan takes it: the partials (lane
+// k < np loads slice k's), a ballot of their bad flags and a sum of their
+// lengths; a sorted batch's span is [offsets[0], offsets[n-1] + lengths[n-1]).
+// lo / hi: the span (dyn).
+__device__ __forceinline__ bool route_region(const Route& r, uint64_t& lo, uint64_t& hi) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint32_t k = min((uint32_t)lane, r.np - 1u);  // (clamped: every load issued)
+  const RoutePart q = r.parts[k];
+  lo = ldc(r.offsets, 0);
+  hi = ldc(r.offsets, r.n - 1u) + ldc(r.lengths, r.n - 1u);
+  const bool mine = (uint32_t)lane < r.np;
+  if (__ballot(mine && q.bad != 0u)) return false;
+  if (!__ballot(mine && q.sum != 0u)) return false;  // nothing to checksum
+  if (!r.dyn) return true;
+  const uint64_t sum = wave_total_u64(mine ? q.sum : 0u);
+  // sorted and non-overlapping: hi - lo >= sum; gaps at most 1/8 of the bytes (+64 KiB)
+  if (hi - lo - sum > sum / 8u + 65536u) return false;
+  const uintptr_t O = ((uintptr_t)r.base + lo) & ~(uintptr_t)(kChunk - 1u);
+  return ((uintptr_t)r.base + hi - O + kChunk - 1u) / kChunk <= r.cap_chunks;
+}
+
 
 // floor(a / d) for wave-uniform a < 2^63, d > 0, from a double-precision
 // estimate (inv_d = 1/d, loop-invariant) corrected by a step or two: the
@@ -1671,12 +1737,18 @@ __device__ bool tile_scan(const G& g, const KArgs& ka, uint8_t* lds) {
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mj = max(mj, (uint32_t)__shfl_xor((int)mj, o));
-  if (lane == 0) wmax[wv] = mj;
-  const bool need = __syncthreads_or(tab ? 1 : 0) != 0;
+  // the wave's largest count, bit 31 = some lane's `tab` (an OR over the
+  // workgroup in the scratch: __syncthreads_or would take 256 B of LDS
+  // beyond the image, which crc32c_route_kernel's region image cannot spare)
+  if (lane == 0) wmax[wv] = mj | (__ballot(tab) ? 0x80000000u : 0u);
+  __syncthreads();
+  bool need = false;
+#pragma unroll
+  for (uint32_t v = 0; v < (uint32_t)NW; ++v) need |= (wmax[v] >> 31) != 0u;
   if (t == 0) {
     uint32_t m = 0;
 #pragma unroll
-    for (uint32_t v = 0; v < (uint32_t)NW; ++v) m = max(m, wmax[v]);
+    for (uint32_t v = 0; v < (uint32_t)NW; ++v) m = max(m, wmax[v] & 0x7FFFFFFFu);
     ka.tiles[2ull * blockIdx.x] = carry;
     ka.tiles[2ull * blockIdx.x + 1] = max(m, 3u);  // head mode: the body kernel has work (> 2, see run_heads)
   }
@@ -2752,6 +2824,10 @@ __device__ const uint16_t* lpt_order(const VarGeom& g, uint8_t* lds, uint64_t i0
 
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(VarGeom gv, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes > kPermLdsBytes ? kFusedLdsBytes : kPermLdsBytes];
+  if (ka.route.parts) {
+    uint64_t lo, hi;
+    if (route_region(ka.route, lo, hi)) return;  // the region path ran
+  }
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1, B0, B1;
   bool long_bufs = false, multi;
@@ -2890,9 +2966,9 @@ constexpr uint32_t kRegionDirect = 64;  // shorter buffers: checksummed whole by
 struct RegionGeom {
   const uint8_t* grid;  // O: chunk c at grid + 4096c
   uint64_t nc;          // chunks
-  uint64_t rel0;        // region - O
-  uint64_t region_len;
-  const uint64_t* offsets;  // from the region start
+  uint64_t rel0;        // buffer i starts at grid position rel0 + offsets[i] (u64, wrapping)
+  uint64_t rs, re;      // the region [rs, re) in grid positions (rs < 4096)
+  const uint64_t* offsets;
   const uint64_t* lengths;
   uint64_t n;
   const uint32_t* init;  // per-buffer Extend seeds (nullptr: init_all)
@@ -2939,7 +3015,7 @@ struct SearchProbe {
   uint64_t w0, e;
 };
 __device__ __forceinline__ SearchProbe region_probe(const RegionGeom& g, uint64_t A, int lane) {
-  const double f = (double)A / (double)(g.rel0 + g.region_len + 1u);
+  const double f = (double)A / (double)(g.re + 1u);
   const uint64_t gi = min((uint64_t)(f * (double)g.n), g.n - 1u);
   const uint64_t w0 = gi > 32u ? gi - 32u : 0u;
   const uint64_t b = min(w0 + (uint64_t)lane, g.n - 1u);
@@ -3186,7 +3262,7 @@ __device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* t
   f.ninit = ~(g.init ? g.init[i] : g.init_all);
   f.s = g.rel0 + off;
   f.L = L;
-  const bool inside = off <= g.region_len && L <= g.region_len - off;
+  const bool inside = f.s >= g.rs && f.s <= g.re && L <= g.re - f.s;
   f.fast = inside && L >= kRegionDirect && (f.s >> 12) >= c0w && ((f.s + L - 1u) >> 12) < B1;
   const uint64_t s = f.fast ? f.s : 0u, e = f.fast ? f.s + L : 64u;  // (the grid's first chunk otherwise)
   const uint64_t c1 = (e - 1u) >> 12;
@@ -3336,13 +3412,13 @@ constexpr uint32_t kSlotReady = 16, kSlotTail = 32, kSlotWaves = 96;
 constexpr uint32_t kRTail = 8;  // single-chunk units at the end of a range (64 / 16 / 8 / 0 A/B'd: DESIGN §3.7)
 
 template <int U>
-__device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds) {
+__device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka, uint8_t* lds, uint32_t G) {
   NVL_TL_DECL();
   NVL_TL(0);
   const int lane = threadIdx.x & 63;
   const uint32_t wv = uniform_u32(threadIdx.x >> 6);
-  const uint64_t B0 = g.nc * blockIdx.x / gridDim.x;
-  const uint64_t B1 = g.nc * (blockIdx.x + 1) / gridDim.x;
+  const uint64_t B0 = g.nc * blockIdx.x / G;  // (G workgroups: blockIdx.x < G)
+  const uint64_t B1 = g.nc * (blockIdx.x + 1) / G;
   const uint32_t cnt = (uint32_t)(B1 - B0);
   const uint32_t nfull = cnt > kRTail ? (cnt - kRTail) / U : 0u;
   const uint32_t nunits = nfull + (cnt - nfull * U);
@@ -3429,7 +3505,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   // the fold; its first unit's loads are in flight meanwhile
   if (wv == 0) {
     const uint64_t Ib = blockIdx.x == 0 ? 0u : (cu ? cursor : region_search(g, B0 * kChunk, lane));
-    const uint64_t Ib1 = blockIdx.x + 1u == gridDim.x ? g.n : region_search(g, B1 * kChunk, lane);
+    const uint64_t Ib1 = blockIdx.x + 1u == G ? g.n : region_search(g, B1 * kChunk, lane);
     const uint64_t sb = Ib < g.n ? g.rel0 + ldg64(g.offsets, Ib) : 0u;
     const uint64_t hc = (Ib < Ib1 && sb < B0 * kChunk) ? B0 - (sb >> 12) : 0u;  // halo chunks
     if (lane == 0) {
@@ -3597,7 +3673,96 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRLdsBytes];
-  run_region<NVL_FAST_U>(g, ka, lds);
+  run_region<NVL_FAST_U>(g, ka, lds, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// Routed batches: one plan, then the region path or the batch path.
+//
+// A batch over device metadata is region-shaped when its buffers are sorted
+// by offset and do not overlap (table/format.cc:90-92 over a table image in
+// file order, db/log_reader.cc:255-256 over a log's records, a packed batch),
+// none is longer than kRegionMaxLen (a longer one would be re-streamed as a
+// halo and folded serially by its owner), and -- for nvl_crc32c_batch_dev,
+// whose region is the batch's own span -- the gaps between them are few
+// bytes against the buffer bytes (the region path reads the gaps).  Only the
+// device knows, so a call is three launches: crc32c_route_plan (partials),
+// crc32c_route_kernel (the region path, or the head kernel's work) and
+// crc32c_var_fused_kernel (returns at once on the region path).
+// Partial k: buffers [n k / P, n (k+1) / P) and each one's successor (four
+// pairs per thread and step, their loads issued together: the plan is a
+// latency-bound scan).  Bad: a pair out of order or overlapping, a length
+// over kRegionMaxLen, a buffer outside [0, lim) (region_dev: lim =
+// region_len; batch_dev: ~0, i.e. only a wrapping end).
+constexpr uint32_t kPlanT = 1024, kPlanPer = 4;
+__global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __restrict__ off,
+                                                           const uint64_t* __restrict__ len, uint64_t n, uint64_t lim,
+                                                           RoutePart* __restrict__ parts) {
+  __shared__ uint64_t wsum[kPlanT / kWave];
+  __shared__ uint32_t wbad[kPlanT / kWave];
+  const uint64_t P = gridDim.x, k = blockIdx.x;
+  const uint64_t i0 = n * k / P, i1 = n * (k + 1) / P;
+  uint64_t sum = 0;  // (lengths capped at kRegionMaxLen + 1: a longer one makes the slice bad anyway)
+  bool bad = false;
+  for (uint64_t b = i0 + (uint64_t)threadIdx.x * kPlanPer; b < i1; b += (uint64_t)kPlanT * kPlanPer) {
+    uint64_t o[kPlanPer + 1], L[kPlanPer];
+#pragma unroll
+    for (uint32_t q = 0; q <= kPlanPer; ++q) o[q] = off[min(b + q, n - 1u)];  // (clamped: every load issued)
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) L[q] = len[min(b + q, n - 1u)];
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) {
+      if (b + q >= i1) break;
+      const uint64_t e = o[q] + L[q];
+      bad |= e < o[q] || L[q] > kRegionMaxLen || o[q] > lim || L[q] > lim - o[q];
+      if (b + q + 1u < n) bad |= e > o[q + 1];
+      sum += min<uint64_t>(L[q], kRegionMaxLen + 1u);
+    }
+  }
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t tot = wave_total_u64(sum);
+  const bool wb = __ballot(bad) != 0u;
+  if (lane == 0u) {
+    wsum[w] = tot;
+    wbad[w] = wb ? 1u : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t s = 0, bb = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < kPlanT / kWave; ++v) {
+      s += wsum[v];
+      bb |= wbad[v];
+    }
+    parts[k] = RoutePart{s, bb};
+  }
+}
+
+// The second launch of a routed call: the region path over the batch (its
+// geometry from the plan for batch_dev), or the head kernel's work.  Launched
+// with one workgroup per CU; the region path runs on the region grid
+// (grid_for), the head work on the plan's tiles; the other workgroups return.
+__global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg, VarGeom vg, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLdsBytes > kRLdsBytes ? kHeadLdsBytes : kRLdsBytes];
+  uint64_t lo, hi;
+  if (route_region(ka.route, lo, hi)) {
+    if (ka.route.dyn) {
+      const uintptr_t base = (uintptr_t)ka.route.base, start = base + lo;
+      const uintptr_t O = start & ~(uintptr_t)(kChunk - 1u);
+      rg.grid = reinterpret_cast<const uint8_t*>(O);
+      rg.rel0 = (uint64_t)(base - O);  // (wrapping: buffer i at rel0 + offsets[i] >= start - O)
+      rg.rs = (uint64_t)(start - O);
+      rg.re = (uint64_t)(base + hi - O);
+      rg.nc = (rg.re + kChunk - 1u) / kChunk;
+    }
+    const uint64_t gw = (rg.nc + kWavesPerWG - 1u) / kWavesPerWG;  // (the host's grid_for)
+    const uint32_t G = (uint32_t)max<uint64_t>(1u, min<uint64_t>(gridDim.x, gw));
+    if (blockIdx.x >= G) return;
+    run_region<NVL_FAST_U>(rg, ka, lds, G);
+  } else {
+    if (blockIdx.x >= ka.tile_G) return;
+    run_heads(vg, ka, lds);
+  }
 }
 
 // Synthetic stream: one thread per 8-byte word.
@@ -3913,12 +4078,100 @@ hipError_t launch_var(const LaunchCtx& lc, const uint8_t* base, const uint64_t* 
   return launch_fixup(recs, grid * dev::kUnitsPerWG, out, flags, lc.stream);
 }
 
+static inline size_t align256(size_t v) { return (v + 255u) / 256u * 256u; }
+
+// A process-wide call generation (never 0, the zeroed workspace's value),
+// seeded at random so that leftover memory is unlikely to hold it: the
+// region fold trusts an event record only when it carries this call's
+// generation AND its own buffer index (workspace memory is never
+// zeroed).
+static uint32_t next_generation() {
+  static std::atomic<uint32_t> s_gen{(uint32_t)std::random_device{}()};
+  uint32_t gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
+  if (gen == 0u) gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
+  return gen;
+}
+
+// Routed calls (crc32c_route_plan -> crc32c_route_kernel -> crc32c_var_fused_kernel).
+size_t route_parts_bytes() { return (dev::kRoutePlanMax * sizeof(dev::RoutePart) + 255u) / 256u * 256u; }
+// Region chunks a region-shaped batch_dev batch can span: sorted, each buffer
+// <= kRegionMaxLen (32 chunks), gaps <= 1/8 of the bytes + 64 KiB -> at most
+// 36 chunks per buffer + 18 + 2 (route_verdict checks it).
+uint64_t route_cap_chunks(uint64_t n) { return 36u * n + 20u; }
+static inline uint32_t route_plan_grid(uint64_t n) {  // one step of 4096 pairs per workgroup up to 64 of them
+  const uint64_t per = (uint64_t)dev::kPlanT * dev::kPlanPer;
+  return (uint32_t)std::min<uint64_t>(dev::kRoutePlanMax, std::max<uint64_t>(1, (n + per - 1u) / per));
+}
+
+hipError_t launch_routed(const LaunchCtx& lc, const uint8_t* base, uint64_t region_len, bool dyn,
+                         const uint64_t* offsets, const uint64_t* lengths, uint64_t n, const uint32_t* init,
+                         uint32_t init_all, uint32_t* out, uint32_t flags, void* region_ws, uint64_t cap_chunks,
+                         void* parts_ws, Rec* recs, uint32_t* hc, uint64_t* lpre, uint64_t* tiles) {
+  if (n == 0) return hipSuccess;
+  if (!lc.counter || !lpre || !tiles || lc.num_cu > (int)dev::kMaxTiles) return hipErrorInvalidValue;
+  const uint32_t P = route_plan_grid(n);
+  dev::RoutePart* parts = static_cast<dev::RoutePart*>(parts_ws);
+  const uint64_t lim = dyn ? ~0ull : region_len;
+  dev::Route rt;
+  rt.parts = parts;
+  rt.np = P;
+  rt.dyn = dyn ? 1u : 0u;
+  rt.base = base;
+  rt.offsets = offsets;
+  rt.lengths = lengths;
+  rt.n = n;
+  rt.cap_chunks = cap_chunks;
+  if (lc.ev_start)
+    hipExtLaunchKernelGGL(dev::crc32c_route_plan, dim3(P), dim3(dev::kPlanT), 0, lc.stream, lc.ev_start, nullptr, 0u,
+                          offsets, lengths, n, lim, parts);
+  else
+    hipLaunchKernelGGL(dev::crc32c_route_plan, dim3(P), dim3(dev::kPlanT), 0, lc.stream, offsets, lengths, n, lim,
+                       parts);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // the region path's geometry: the caller's region, or (dyn) set in the kernel from the plan
+  uint8_t* w = static_cast<uint8_t*>(region_ws);
+  uint32_t* raws = reinterpret_cast<uint32_t*>(w);
+  uint4* qs = reinterpret_cast<uint4*>(w + align256(cap_chunks * 4u));
+  uint4* qe = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 16u));
+  const uintptr_t O = dyn ? 0u : (uintptr_t)base & ~(uintptr_t)(dev::kChunk - 1u);
+  const uint64_t rel0 = dyn ? 0u : (uintptr_t)base - O;
+  const uint64_t nc = dyn ? 0u : (rel0 + region_len + dev::kChunk - 1u) / dev::kChunk;
+  dev::RegionGeom rg{reinterpret_cast<const uint8_t*>(O), nc, rel0, rel0, rel0 + region_len, offsets, lengths, n,
+                     init, init_all, raws, qs, qe, next_generation()};
+  const dev::VarGeom vg{base, offsets, lengths, nullptr, nullptr, n, init, init_all};
+  const uint32_t hg = head_grid(lc.num_cu, n);
+  dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, hc};
+  ka.lpre = lpre;
+  ka.tiles = tiles;
+  ka.tile_G = hg;
+  ka.tile_S = (n + hg - 1) / hg;
+  ka.short_ok = 1u;
+  ka.route = rt;
+  hipLaunchKernelGGL(dev::crc32c_route_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kThreads), 0, lc.stream, rg, vg,
+                     ka);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  dev::KArgs kf{out, flags, recs, lc.tables, lc.counter, hc};
+  kf.lpre = lpre;
+  kf.tiles = tiles;
+  kf.tile_G = hg;
+  kf.tile_S = ka.tile_S;
+  kf.route = rt;
+  if (lc.ev_stop)
+    hipExtLaunchKernelGGL(dev::crc32c_var_fused_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kWave * dev::kGenWaves),
+                          0, lc.stream, nullptr, lc.ev_stop, 0u, vg, kf);
+  else
+    hipLaunchKernelGGL(dev::crc32c_var_fused_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kWave * dev::kGenWaves), 0,
+                       lc.stream, vg, kf);
+  return hipGetLastError();
+}
+
 // Region workspace: [raws: chunks u32][qs: n x 8 B][qe: n x 8 B] (chunks bounded
 // by region_len / 4096 + 2 whatever the region's alignment).
-static inline size_t align256(size_t v) { return (v + 255u) / 256u * 256u; }
-size_t region_ws_bytes(uint64_t region_len, uint64_t n) {
-  return align256((region_len / dev::kChunk + 2u) * 4u) + 2u * align256(n * 16u);
-}
+size_t region_ws_bytes_cap(uint64_t cap_chunks, uint64_t n) { return align256(cap_chunks * 4u) + 2u * align256(n * 16u); }
+uint64_t region_cap_chunks(uint64_t region_len) { return region_len / dev::kChunk + 2u; }
+size_t region_ws_bytes(uint64_t region_len, uint64_t n) { return region_ws_bytes_cap(region_cap_chunks(region_len), n); }
 
 hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t region_len, const uint64_t* offsets,
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
@@ -3931,14 +4184,8 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
   uint32_t* raws = reinterpret_cast<uint32_t*>(w);
   uint4* qs = reinterpret_cast<uint4*>(w + align256((region_len / dev::kChunk + 2u) * 4u));
   uint4* qe = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(qs) + align256(n * 16u));
-  // A process-wide call generation (never 0, the zeroed workspace's value),
-  // seeded at random so that leftover memory is unlikely to hold it: the
-  // fold trusts an event record only when it carries this call's generation
-  // AND its own buffer index (workspace memory is never zeroed).
-  static std::atomic<uint32_t> s_gen{(uint32_t)std::random_device{}()};
-  uint32_t gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
-  if (gen == 0u) gen = s_gen.fetch_add(1u, std::memory_order_relaxed) + 1u;
-  dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, region_len, offsets, lengths, n, init, init_all,
+  const uint32_t gen = next_generation();
+  dev::RegionGeom g{reinterpret_cast<const uint8_t*>(O), nc, rel0, rel0, rel0 + region_len, offsets, lengths, n, init, init_all,
                     raws, qs, qe, gen};
   dev::KArgs ka{out, flags, nullptr, lc.tables, nullptr, nullptr};
   const uint32_t grid = grid_for(lc.num_cu, nc);  // >= 1 (nc >= 1: n > 0 buffers inside the region)

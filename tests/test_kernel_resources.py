@@ -42,14 +42,15 @@ def usage(tmp_path_factory):
 
 HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_var_kernel", "crc32c_var_fused_kernel",
        "crc32c_region_kernel", "crc32c_chunks_kernel",
-       "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel"]
+       "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel", "crc32c_route_kernel", "crc32c_route_plan"]
 # SGPR spills go to VGPR lanes (v_writelane/v_readlane), not memory: a bound
 # per kernel so that a jump shows.  The fused kernel parks plan-phase scalars
 # there; the variable-length kernels keep scheduler C's two chunk positions
 # (current pair, next pair) in SGPRs; the head kernel keeps two items'
 # metadata (current, next) live in SGPRs while the next-but-one's loads are in
 # flight.
-SGPR_SPILL_MAX = {"crc32c_var_fused_kernel": 48, "crc32c_var_kernel": 48, "crc32c_head_kernel": 160}
+SGPR_SPILL_MAX = {"crc32c_var_fused_kernel": 48, "crc32c_var_kernel": 48, "crc32c_head_kernel": 160,
+                  "crc32c_route_kernel": 48}  # (the head kernel's and the region kernel's scalars in one kernel)
 
 
 @pytest.mark.parametrize("name", HOT)

@@ -2,7 +2,11 @@
 around each call, median of R reps), every result checked.
     python tools/bench_configs.py [--lib build/libnvl_crc32c_X.so] [--configs 2,3,4,v,g,r]
   2, 3, 4  BASELINE configs 2-4 (golden digests)
-  3R, vR, rR  config 3, v and r through nvl_crc32c_region_dev (the region path)
+  3R, vR, rR  config 3, v and r through nvl_crc32c_region_dev (layout checked on the device: plan,
+           region path, the body kernel's early exit)
+  3S, vS, rS  the same with NVL_CRC32C_FLAG_REGION_SHAPED (the region kernel alone, one launch)
+  u, uR    10^5 x 4 KiB at 4 KiB-aligned offsets in a random order (not region-shaped) through
+           nvl_crc32c_batch_dev / nvl_crc32c_region_dev (both: plan, then the batch kernels)
   big1     one aligned 1 GiB buffer (fixed path, n = 1)
   v        10^5 x 4097 B at stride 4101: block | type of 4096-byte SSTable blocks with their
            4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
@@ -11,7 +15,8 @@ around each call, median of R reps), every result checked.
   q        10^5 x 3500 B packed at stride 3500: the same, some starts in a page's first granule
   r        10^5 buffers of 3364..4109 B (the n+1 of data blocks at block_size 4096)
            at stride length+4, nvl_crc32c_batch_dev
-v, g and r are checked CRC by CRC against the oracle."""
+  3, v and r through nvl_crc32c_batch_dev are region-shaped: routed to the region path.
+v, g, r and u are checked CRC by CRC against the oracle."""
 import argparse, time, ctypes, json, os, sys
 import numpy as np, torch
 ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -63,7 +68,7 @@ def timeit(fn, reps):
     return float(np.median([ev[2*j].elapsed_time(ev[2*j+1]) for j in range(reps)])) * 1e-3
 
 
-def varlen(offs, lens, total, seed, region=False):
+def varlen(offs, lens, total, seed, region=False, shaped=False):
     n = lens.size
     buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
     lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, seed, None)
@@ -72,8 +77,9 @@ def varlen(offs, lens, total, seed, region=False):
     if region:  # nvl_crc32c_region_dev over the region [buf, buf + total)
         wsb = lib.nvl_crc32c_region_workspace_bytes(total, n)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        fl = _lib.FLAG_REGION_SHAPED if shaped else 0
         fn = lambda: lib.nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.data_ptr(), None, 0,
-                                               out.data_ptr(), n, 0, ws.data_ptr(), wsb, st)
+                                               out.data_ptr(), n, fl, ws.data_ptr(), wsb, st)
         return buf, out, fn, (o, m, ws)
     wsb = lib.nvl_crc32c_batch_workspace_bytes(n)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
@@ -105,23 +111,29 @@ for c in a.configs.split(","):
         alg = L + 4
         want = p.fixed(buf.cpu().numpy(), L, L, 1)
         check = lambda res: bool(np.array_equal(res, want))
-    elif c in ("3", "3R"):
+    elif c in ("3", "3R", "3S"):
         cfg = g["cfg3"]; total = cfg["total"]
         lens = p.cfg3_lengths(cfg["len_seed"], total)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
         n = lens.size
-        buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"], region=c == "3R")
+        buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"], region=c != "3", shaped=c == "3S")
         alg = total + 12 * n
         check = lambda res: p.digest(res) == cfg["digest"]
-    elif c in ("v", "r", "vR", "rR"):
+    elif c in ("v", "r", "vR", "rR", "vS", "rS", "u", "uR"):
         n = 100_000
         if c[0] == "v":
             lens = np.full(n, 4097, dtype=np.int64)
+        elif c[0] == "u":
+            lens = np.full(n, 4096, dtype=np.int64)
         else:
             lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
-        offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
-        total = int(offs[-1] + lens[-1]) + 4
-        buf, out, fn, keep = varlen(offs, lens, total, 0x5EED00B1, region=c.endswith("R"))
+        if c[0] == "u":
+            offs = np.random.default_rng(8).permutation(n).astype(np.int64) * 4096
+            total = n * 4096
+        else:
+            offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
+            total = int(offs[-1] + lens[-1]) + 4
+        buf, out, fn, keep = varlen(offs, lens, total, 0x5EED00B1, region=c[1:] in ("R", "S"), shaped=c[1:] == "S")
         alg = int(lens.sum()) + 20 * n
         host = buf.cpu().numpy()
         check = lambda res: bool(np.array_equal(res, p.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64))))

@@ -29,8 +29,8 @@ The JSON line adds
                   (HIP events on the launch stream around the K launches / K),
                   against the 8 TB/s HBM3E peak.  `traffic` is the committed
                   PMC-measured HBM bytes per launch (profiles/pmc_traffic.json,
-                  rocprofv3 --pmc passes, corrected per MI355X_MICROARCH.md
-                  §HBM), labelled as such, else null.
+                  rocprofv3 --pmc passes: L2 memory-side request counts by
+                  size, MI355X_MICROARCH.md §HBM), labelled as such, else null.
   cfg5         -- BASELINE config 5 on the same N ranks (every run, N = 1
                   included): 10^7 x 4 KiB blocks in total round-robin over
                   the N GPUs (strong scaling), its GiB/s, frac, and every
@@ -668,8 +668,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(frac, 4), "traffic": traffic,
                          "traffic_source": (f"committed PMC, not measured in this run: profiles/pmc_traffic.json "
-                                            f"({traffic_src}; rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
-                                            f"this kernel and batch, gfx950 corrections per MI355X_MICROARCH.md)"
+                                            f"({traffic_src}; rocprofv3 --pmc passes over this kernel and batch: "
+                                            f"L2 memory-side request counts by size, FETCH_SIZE x 2 / WRITE_SIZE "
+                                            f"beside, per MI355X_MICROARCH.md § HBM)"
                                             if traffic is not None else None),
                          "kernel": kern, "alg_bytes_per_launch": alg_bytes,
                          "mean_kernel_us": round(period_s * 1e6, 2),

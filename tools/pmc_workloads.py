@@ -3,9 +3,11 @@ tools/pmc.sh output directories (one per workload).
     python tools/pmc_workloads.py OUT.json name=DIR:ALG_BYTES:kernel1,kernel2 ...
 Every counter is the mean per dispatch over the workload's timed launches,
 scaled by launched waves (Grid_Size / 64) / SQ_WAVES (the share of SQ
-instances the counters sample); HBM read = FETCH_SIZE kB x 2 (gfx950 half
-count on 16-B/lane streams) x 1024, write = WRITE_SIZE kB x 1024
-(/opt/skills/guides/MI355X_MICROARCH.md)."""
+instances the counters sample); HBM read = 64 B x TCC_EA0_RDREQ + 64 B x
+TCC_EA0_RDREQ_128B (a 128-B request counts twice), write = 32 B x
+TCC_EA0_WRREQ + 32 B x TCC_EA0_WRREQ_64B; FETCH_SIZE kB x 2 x 1024 (the
+gfx950 half count on 16-B/lane streams) and WRITE_SIZE kB x 1024 beside
+(/opt/skills/guides/MI355X_MICROARCH.md § HBM)."""
 import csv, glob, json, os, sys
 from collections import defaultdict
 
@@ -46,10 +48,21 @@ for spec in sys.argv[2:]:
         c = kernel_counters(d, k)
         rec = {x: round(c[x]) for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT",
                                         "SQ_LDS_IDX_ACTIVE") if x in c}
+        # HBM bytes from the L2's memory-side request counts by request size
+        # (read requests are 64 B or 128 B, write requests 32 B or 64 B):
+        # valid for any access width, unlike FETCH_SIZE x 2, which holds for
+        # wide coalesced 16-B/lane streams only (MI355X_MICROARCH.md § HBM);
+        # FETCH_SIZE x 2 / WRITE_SIZE kept beside as the cross-check
+        if "TCC_EA0_RDREQ_sum" in c and "TCC_EA0_RDREQ_128B_sum" in c:
+            rec["hbm_read_bytes"] = round(64 * c["TCC_EA0_RDREQ_sum"] + 64 * c["TCC_EA0_RDREQ_128B_sum"])
+        if "TCC_EA0_WRREQ_sum" in c and "TCC_EA0_WRREQ_64B_sum" in c:
+            rec["hbm_write_bytes"] = round(32 * c["TCC_EA0_WRREQ_sum"] + 32 * c["TCC_EA0_WRREQ_64B_sum"])
         if "FETCH_SIZE" in c:
-            rec["hbm_read_bytes"] = round(c["FETCH_SIZE"] * 2 * 1024)
+            rec["fetch_size_x2_bytes"] = round(c["FETCH_SIZE"] * 2 * 1024)
+            rec.setdefault("hbm_read_bytes", rec["fetch_size_x2_bytes"])
         if "WRITE_SIZE" in c:
-            rec["hbm_write_bytes"] = round(c["WRITE_SIZE"] * 1024)
+            rec["write_size_bytes"] = round(c["WRITE_SIZE"] * 1024)
+            rec.setdefault("hbm_write_bytes", rec["write_size_bytes"])
         w["kernels"][k] = rec
         for x, v in rec.items():
             tot[x] += v

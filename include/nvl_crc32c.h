@@ -203,6 +203,27 @@ NVL_API int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len
                                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all,
                                          uint32_t* out, uint64_t n, uint32_t flags);
 
+/* Several devices, host-resident (the compaction output of db/db_impl.cc:920-923
+ * or an mmap'd table scan, util/env_posix.cc:199-209, over the GPUs of a node):
+ * the batch is cut into at most ndev contiguous index ranges of about equal
+ * covered bytes -- no more than (bytes / min_bytes_per_device) of them, so a
+ * small batch stays on devices[0] -- and range k runs as
+ * nvl_crc32c_batch_region_host on devices[k] (its own pinned staging, stream
+ * and PCIe link) from a pool thread, results written straight into out.
+ * min_bytes_per_device = 0: NVL_CRC32C_MULTI_MIN_BYTES.  A device may appear
+ * twice (two pipes into one GPU).  Synchronous; multi calls are serialised. */
+#define NVL_CRC32C_MULTI_MIN_BYTES (64ull << 20)
+NVL_API int nvl_crc32c_batch_region_host_multi(const void* region, uint64_t region_len, const uint64_t* offsets,
+                                               const uint64_t* lengths, const uint32_t* init, uint32_t init_all,
+                                               uint32_t* out, uint64_t n, uint32_t flags, const int* devices,
+                                               int ndev, uint64_t min_bytes_per_device);
+
+/* The cut nvl_crc32c_batch_region_host_multi makes: part k is buffers
+ * [part_first[k], part_first[k+1]) (part_first holds ndev + 1 entries);
+ * returns the number of parts (>= 1), or a negative status. */
+NVL_API int nvl_crc32c_multi_plan(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, int ndev,
+                                  uint64_t min_bytes, uint64_t* part_first);
+
 /* Host fixed-stride batch (one contiguous host region, e.g. an mmap'd table
  * file or a pinned bench buffer), pipelined H2D/compute/D2H over two
  * streams.  Synchronous. */

@@ -332,6 +332,51 @@ def extend_fixed_host(buf: np.ndarray, stride: int, length: int, n: int, init=0,
     return out
 
 
+def extend_region_host(region: np.ndarray, offsets, lengths, init=0, *, mask: bool = False,
+                       devices: Optional[Sequence[int]] = None, min_bytes_per_device: int = 0) -> np.ndarray:
+    """out[i] = Extend(init_i, region[offsets[i] : offsets[i] + lengths[i]]) for
+    buffers in ONE host region (an mmap'd file image, a log block run):
+    nvl_crc32c_batch_region_host on the current device, or with ``devices``
+    nvl_crc32c_batch_region_host_multi -- contiguous ranges of the batch on
+    those devices at once, each over its own PCIe link (synchronous)."""
+    a = region if isinstance(region, np.ndarray) else np.frombuffer(region, dtype=np.uint8)
+    a = np.ascontiguousarray(a).view(np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    m = np.ascontiguousarray(lengths, dtype=np.uint64)
+    n = o.size
+    if m.size != n:
+        raise ValueError("offsets and lengths differ in size")
+    out = np.empty(n, dtype=np.uint32)
+    init_ptr, init_all = None, 0
+    if isinstance(init, int):
+        init_all = init & 0xFFFFFFFF
+    else:
+        ini = np.ascontiguousarray(np.asarray(init, dtype=np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
+        init_ptr = ini.ctypes.data
+    flags = FLAG_MASK if mask else 0
+    if devices is None:
+        rc = lib.nvl_crc32c_batch_region_host(a.ctypes.data, a.nbytes, o.ctypes.data, m.ctypes.data, init_ptr,
+                                              init_all, out.ctypes.data, n, flags)
+        check(rc, "nvl_crc32c_batch_region_host")
+    else:
+        dv = np.ascontiguousarray(devices, dtype=np.int32)
+        rc = lib.nvl_crc32c_batch_region_host_multi(a.ctypes.data, a.nbytes, o.ctypes.data, m.ctypes.data, init_ptr,
+                                                    init_all, out.ctypes.data, n, flags, dv.ctypes.data, dv.size,
+                                                    min_bytes_per_device)
+        check(rc, "nvl_crc32c_batch_region_host_multi")
+    return out
+
+
+def multi_plan(offsets, lengths, ndev: int, min_bytes: int = 0) -> np.ndarray:
+    """nvl_crc32c_multi_plan: the first buffer of each part (+ n at the end)."""
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    m = np.ascontiguousarray(lengths, dtype=np.uint64)
+    first = np.zeros(ndev + 1, dtype=np.uint64)
+    k = lib.nvl_crc32c_multi_plan(o.ctypes.data, m.ctypes.data, o.size, ndev, min_bytes, first.ctypes.data)
+    check(k if k < 0 else 0, "nvl_crc32c_multi_plan")
+    return first[:k + 1]
+
+
 def fill_splitmix(buf, nblocks: int, block_bytes: int, seed: int, *, first_block: int = 0,
                   block_step: int = 1) -> None:
     """Write the canonical synthetic stream into a device tensor:
@@ -352,4 +397,5 @@ def to_u32(t) -> np.ndarray:
 
 __all__ = ["extend", "value", "mask", "unmask", "kMaskDelta", "init", "gpu_accelerated",
            "extend_fixed", "FixedBatch", "extend_batch", "extend_region", "extend_batch_host", "extend_fixed_host",
-           "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix", "to_u32", "Crc32cError"]
+           "extend_region_host", "multi_plan", "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix",
+           "to_u32", "Crc32cError"]

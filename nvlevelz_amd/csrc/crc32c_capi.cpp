@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -910,6 +912,127 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   (void)hipFreeAsync(d, st);
   if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
+}
+
+// ---- several devices, host-resident ----------------------------------------
+// nvl_crc32c_batch_region_host_multi: the batch in contiguous index ranges of
+// about equal covered bytes, one per device, each staged and checksummed by
+// nvl_crc32c_batch_region_host on its device from its own thread (its own
+// pinned staging, stream and PCIe link), results straight into out.  Part 0
+// runs on the calling thread; the others on a pool of persistent worker
+// threads (their staging survives between calls).  Multi calls are
+// serialised on the pool.
+
+int nvl_crc32c_multi_plan(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, int ndev,
+                          uint64_t min_bytes, uint64_t* part_first) {
+  if (!offsets || !lengths || !part_first || ndev <= 0) return NVL_CRC32C_EINVAL;
+  if (min_bytes == 0) min_bytes = NVL_CRC32C_MULTI_MIN_BYTES;
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) total += lengths[i];
+  uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ndev, total / min_bytes));
+  if (parts > n) parts = std::max<uint64_t>(1, n);
+  // cut where the running byte count crosses k * total / parts
+  part_first[0] = 0;
+  uint64_t k = 1, acc = 0;
+  for (uint64_t i = 0; i < n && k < parts; ++i) {
+    acc += lengths[i];
+    while (k < parts && acc >= (total / parts) * k && i + 1 < n) part_first[k++] = i + 1;
+  }
+  while (k < parts) part_first[k++] = n;  // (degenerate: fewer cuts than parts)
+  part_first[parts] = n;
+  return (int)parts;
+}
+
+namespace {
+struct MultiPool {
+  struct Worker {
+    std::mutex m;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool busy = false;
+  };
+  std::mutex call_mu;  // one multi call at a time
+  std::mutex mu;
+  std::vector<Worker*> workers;
+  Worker* get(size_t k) {
+    std::lock_guard<std::mutex> lk(mu);
+    while (workers.size() <= k) {
+      Worker* w = new Worker;
+      std::thread([w] {
+        for (;;) {
+          std::function<void()> j;
+          {
+            std::unique_lock<std::mutex> lk2(w->m);
+            w->cv.wait(lk2, [w] { return w->busy && w->job; });
+            j = std::move(w->job);
+            w->job = nullptr;
+          }
+          j();
+          {
+            std::lock_guard<std::mutex> lk2(w->m);
+            w->busy = false;
+          }
+          w->cv.notify_all();
+        }
+      }).detach();  // (idle at exit; never joined: the HIP runtime may already be gone)
+      workers.push_back(w);
+    }
+    return workers[k];
+  }
+  void run(Worker* w, std::function<void()> j) {
+    std::lock_guard<std::mutex> lk(w->m);
+    w->job = std::move(j);
+    w->busy = true;
+    w->cv.notify_all();
+  }
+  void wait(Worker* w) {
+    std::unique_lock<std::mutex> lk(w->m);
+    w->cv.wait(lk, [w] { return !w->busy; });
+  }
+};
+MultiPool& multi_pool() {
+  static MultiPool* p = new MultiPool;  // (leaked on purpose: detached workers hold it)
+  return *p;
+}
+}  // namespace
+
+int nvl_crc32c_batch_region_host_multi(const void* region, uint64_t region_len, const uint64_t* offsets,
+                                       const uint64_t* lengths, const uint32_t* init, uint32_t init_all,
+                                       uint32_t* out, uint64_t n, uint32_t flags, const int* devices, int ndev,
+                                       uint64_t min_bytes_per_device) {
+  if (n == 0) return NVL_CRC32C_OK;
+  if (!devices || ndev <= 0 || ndev > 64) return NVL_CRC32C_EINVAL;
+  if (!offsets || !lengths || !out || (!region && region_len)) return NVL_CRC32C_EINVAL;
+  std::vector<uint64_t> first((size_t)ndev + 1);
+  const int parts = nvl_crc32c_multi_plan(offsets, lengths, n, ndev, min_bytes_per_device, first.data());
+  if (parts < 0) return parts;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  auto part = [&](int k) -> int {
+    if (hipSetDevice(devices[k]) != hipSuccess) return NVL_CRC32C_ENODEV;
+    const uint64_t a = first[k], b = first[k + 1];
+    return nvl_crc32c_batch_region_host(region, region_len, offsets + a, lengths + a, init ? init + a : nullptr,
+                                        init_all, out + a, b - a, flags);
+  };
+  if (parts == 1) {
+    const int rc = part(0);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+  }
+  MultiPool& pool = multi_pool();
+  std::lock_guard<std::mutex> call(pool.call_mu);
+  std::vector<int> rc((size_t)parts, NVL_CRC32C_OK);
+  std::vector<MultiPool::Worker*> ws((size_t)parts, nullptr);
+  for (int k = 1; k < parts; ++k) {
+    ws[k] = pool.get((size_t)k - 1);
+    pool.run(ws[k], [&, k] { rc[k] = part(k); });
+  }
+  rc[0] = part(0);
+  for (int k = 1; k < parts; ++k) pool.wait(ws[k]);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  for (int k = 0; k < parts; ++k)
+    if (rc[k] != NVL_CRC32C_OK) return rc[k];
+  return NVL_CRC32C_OK;
 }
 
 int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,

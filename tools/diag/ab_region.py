@@ -38,6 +38,8 @@ outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
 wsb = libs[0].nvl_crc32c_region_workspace_bytes(total, n)
 ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 st = torch.cuda.current_stream().cuda_stream
+# NVL_CRC32C_FLAG_REGION_SHAPED by default: the region kernel alone (AB_FLAGS=0: the routed call)
+FLAGS = int(os.environ.get("AB_FLAGS", "2"))
 nfix = 100_000  # the config-2 reference (fixed path, first library) timed in the same rounds
 fbuf = torch.empty(nfix * 4096, dtype=torch.uint8, device=dev)
 libs[0].nvl_crc32c_fill_splitmix(fbuf.data_ptr(), nfix, 4096, 0, 1, 0x5EED0001, None)
@@ -49,7 +51,7 @@ def run(k):
         return libs[0].nvl_crc32c_fixed_dev(fbuf.data_ptr(), 4096, 4096, nfix, None, 0, fout.data_ptr(), 0, None, 0,
                                             st)
     return libs[k].nvl_crc32c_region_dev(buf.data_ptr(), total, o.data_ptr(), m.data_ptr(), None, 0,
-                                         outs[k].data_ptr(), n, 0, ws.data_ptr(), wsb, st)
+                                         outs[k].data_ptr(), n, FLAGS, ws.data_ptr(), wsb, st)
 rounds, reps = int(os.environ.get("AB_ROUNDS", "10")), int(os.environ.get("AB_REPS", "30"))
 per = [[] for _ in range(len(libs) + 1)]
 single = [[] for _ in range(len(libs) + 1)]

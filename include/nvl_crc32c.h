@@ -108,6 +108,12 @@ NVL_API uint32_t nvl_crc32c_mask(uint32_t crc);
 /* util/crc32c.h:37-40 leveldb::crc32c::Unmask */
 NVL_API uint32_t nvl_crc32c_unmask(uint32_t masked_crc);
 
+/* Which host implementation the single-buffer calls use (chosen once, after
+ * a known-answer self-test, like util/crc32c.cc:290-303): "avx512 vpclmulqdq
+ * fold + sse4.2", "sse4.2 crc32q x3" or "slice-by-8".  The environment
+ * variable NVL_CRC32C_HOST=sse|table caps the tier (tests). */
+NVL_API const char* nvl_crc32c_host_impl(void);
+
 /* ---- batched, device-resident (the hot path) ----------------------------- */
 
 /* Fixed-stride batch: buffer i is the `len` bytes at base + i*stride (device

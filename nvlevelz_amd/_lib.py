@@ -42,6 +42,7 @@ SIGNATURES = {
     "nvl_crc32c_gpu_accelerated": (_int, []),
     "nvl_crc32c_strerror": (_c.c_char_p, [_int]),
     "nvl_crc32c_abi_version": (_int, []),
+    "nvl_crc32c_host_impl": (_c.c_char_p, []),
     "nvl_crc32c_extend": (_u32, [_u32, _vp, _sz]),
     "nvl_crc32c_value": (_u32, [_vp, _sz]),
     "nvl_crc32c_mask": (_u32, [_u32]),

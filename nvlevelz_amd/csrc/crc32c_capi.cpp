@@ -685,6 +685,8 @@ uint32_t nvl_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
 
 uint32_t nvl_crc32c_value(const void* data, size_t n) { return host_extend(0, data, n); }
 
+const char* nvl_crc32c_host_impl(void) { return host_impl_name(); }
+
 uint32_t nvl_crc32c_mask(uint32_t crc) { return nvl::mask(crc); }
 
 uint32_t nvl_crc32c_unmask(uint32_t masked_crc) { return nvl::unmask(masked_crc); }

@@ -153,7 +153,8 @@ size_t scan_temp_bytes(uint64_t n);
 hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
                               hipStream_t st);
 
-// CPU single-buffer Extend (crc32c_host.cpp).
+// CPU single-buffer Extend (crc32c_host.cpp) and the tier it chose.
 uint32_t host_extend(uint32_t init, const void* data, size_t n);
+const char* host_impl_name();
 
 }  // namespace nvl

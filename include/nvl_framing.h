@@ -34,7 +34,7 @@ extern "C" {
  * batches of fewer than nvl_framing_gpu_min_bytes() checksummed bytes run on
  * the calling thread's host CRC (nvl_crc32c_extend), larger ones on the GPU
  * (one staging copy, H2D, one batch kernel, D2H) -- the crossover measured at
- * the fork's call-site sizes (profiles/r04_shim_latency.jsonl);
+ * the fork's call-site sizes (profiles/r05_shim_latency.jsonl);
  * the environment variable NVL_FRAMING_GPU_MIN_BYTES overrides it.  The two
  * flags force an engine.  A GPU batch that fails returns its error; no call
  * ever falls back to the other engine.  (nvl_sstable_verify_table_dev's image

@@ -17,9 +17,12 @@
 #include "nvl_framing.h"
 
 // flags = 0 crossover (bytes checksummed per host-resident call), from
-// profiles/r04_shim_latency.jsonl.
+// profiles/r05_shim_latency.jsonl: with the AVX-512 folding
+// host CRC the host wins at 32 MiB (0.84-1.08 vs 1.49-1.51 ms), the GPU at
+// 128 MiB (3.26-3.66 vs 5.29-5.70 ms); round 4's SSE4.2 host CRC crossed at
+// ~17 MiB.
 #ifndef NVL_FRAMING_DEFAULT_GPU_MIN_BYTES
-#define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES (16ull << 20)  // host wins below ~17 MiB, GPU from 32 MiB
+#define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES (64ull << 20)
 #endif
 
 namespace nvl {

@@ -133,6 +133,12 @@ def test_config3_full(dev, C, port):
     assert port.digest(got) == g["digest"]
     want = port.varlen(buf.cpu().numpy(), offs.astype(np.uint64), lens)
     assert np.array_equal(got, want)
+    # The same buffers in a random order: not region-shaped, so
+    # nvl_crc32c_batch_dev's route runs the batch kernels (head + body) at
+    # full config-3 size -- the packed order above takes the region path.
+    perm = np.random.default_rng(3).permutation(lens.size)
+    got_p = _varlen(C, dev, buf, offs[perm], lens.astype(np.int64)[perm])
+    assert np.array_equal(got_p, want[perm])
 
 
 def test_config4_full(dev, C, port):

@@ -3684,8 +3684,9 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g
 // file order, db/log_reader.cc:255-256 over a log's records, a packed batch),
 // none is longer than kRegionMaxLen (a longer one would be re-streamed as a
 // halo and folded serially by its owner), and -- for nvl_crc32c_batch_dev,
-// whose region is the batch's own span -- the gaps between them are few
-// bytes against the buffer bytes (the region path reads the gaps).  Only the
+// whose region is the batch's own span -- no page of the span is without a
+// buffer byte and the gaps are few bytes against the buffer bytes (the
+// region path reads the gaps).  Only the
 // device knows, so a call is three launches: crc32c_route_plan (partials),
 // crc32c_route_kernel (the region path, or the head kernel's work) and
 // crc32c_var_fused_kernel (returns at once on the region path).
@@ -3693,10 +3694,20 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g
 // pairs per thread and step, their loads issued together: the plan is a
 // latency-bound scan).  Bad: a pair out of order or overlapping, a length
 // over kRegionMaxLen, a buffer outside [0, lim) (region_dev: lim =
-// region_len; batch_dev: ~0, i.e. only a wrapping end).
+// region_len; batch_dev: ~0, i.e. only a wrapping end).  batch_dev (`pages`)
+// also: a 4 KiB page of the batch's span that holds no buffer byte -- the
+// region path reads every page of the span, and only the pages a buffer
+// touches are known to be mapped (two buffers from different allocations
+// may have an unmapped page between them).  Page-wise, in address space
+// (A(x) = base + x): a non-empty buffer starts at most one page after the
+// page of the previous buffer's last byte, an empty one no later than that
+// byte's page ends (page(A(o) - 1) <= page(A(e_prev) - 1)), and the first
+// buffer is not empty -- so the last byte's page of every prefix is touched
+// and no page is skipped.
 constexpr uint32_t kPlanT = 1024, kPlanPer = 4;
 __global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __restrict__ off,
                                                            const uint64_t* __restrict__ len, uint64_t n, uint64_t lim,
+                                                           uintptr_t base, uint32_t pages,
                                                            RoutePart* __restrict__ parts) {
   __shared__ uint64_t wsum[kPlanT / kWave];
   __shared__ uint32_t wbad[kPlanT / kWave];
@@ -3705,17 +3716,26 @@ __global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __re
   uint64_t sum = 0;  // (lengths capped at kRegionMaxLen + 1: a longer one makes the slice bad anyway)
   bool bad = false;
   for (uint64_t b = i0 + (uint64_t)threadIdx.x * kPlanPer; b < i1; b += (uint64_t)kPlanT * kPlanPer) {
-    uint64_t o[kPlanPer + 1], L[kPlanPer];
+    uint64_t o[kPlanPer + 1], L[kPlanPer + 1];
 #pragma unroll
     for (uint32_t q = 0; q <= kPlanPer; ++q) o[q] = off[min(b + q, n - 1u)];  // (clamped: every load issued)
 #pragma unroll
-    for (uint32_t q = 0; q < kPlanPer; ++q) L[q] = len[min(b + q, n - 1u)];
+    for (uint32_t q = 0; q <= kPlanPer; ++q) L[q] = len[min(b + q, n - 1u)];
 #pragma unroll
     for (uint32_t q = 0; q < kPlanPer; ++q) {
       if (b + q >= i1) break;
       const uint64_t e = o[q] + L[q];
       bad |= e < o[q] || L[q] > kRegionMaxLen || o[q] > lim || L[q] > lim - o[q];
-      if (b + q + 1u < n) bad |= e > o[q + 1];
+      if (b + q + 1u < n) {
+        bad |= e > o[q + 1];
+        if (pages) {
+          const bool nz = L[q + 1] != 0u;
+          const uint64_t pn = ((uint64_t)base + o[q + 1] - (nz ? 0u : 1u)) >> 12;
+          const uint64_t pe = ((uint64_t)base + e - 1u) >> 12;
+          bad |= pn > pe + (nz ? 1u : 0u);
+        }
+      }
+      if (pages && b + q == 0u) bad |= L[q] == 0u;
       sum += min<uint64_t>(L[q], kRegionMaxLen + 1u);
     }
   }
@@ -4123,10 +4143,10 @@ hipError_t launch_routed(const LaunchCtx& lc, const uint8_t* base, uint64_t regi
   rt.cap_chunks = cap_chunks;
   if (lc.ev_start)
     hipExtLaunchKernelGGL(dev::crc32c_route_plan, dim3(P), dim3(dev::kPlanT), 0, lc.stream, lc.ev_start, nullptr, 0u,
-                          offsets, lengths, n, lim, parts);
+                          offsets, lengths, n, lim, (uintptr_t)base, dyn ? 1u : 0u, parts);
   else
     hipLaunchKernelGGL(dev::crc32c_route_plan, dim3(P), dim3(dev::kPlanT), 0, lc.stream, offsets, lengths, n, lim,
-                       parts);
+                       (uintptr_t)base, dyn ? 1u : 0u, parts);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the region path's geometry: the caller's region, or (dyn) set in the kernel from the plan

@@ -651,3 +651,66 @@ def region_span_stale(u: int, B0: int, nfull: int, nunits: int, nhalo: int, hc: 
         return region_span(u, B0, nfull, nunits, B0, 0, U)
     h = u - nunits
     return B0 + h * U, (min(U, hc - h * U) if h < nhalo else 0)
+
+
+# ---- routed calls: the plan's verdict (crc32c_kernels.hip crc32c_route_plan,
+# route_region) ------------------------------------------------------------
+REGION_MAX_LEN = 128 << 10
+
+
+def route_plan_bad(offs, lens, lim: int, base: int, pages: bool) -> bool:
+    """The plan's bad flag over the whole batch (the OR of its partials):
+    pairs out of order / overlapping, a length over REGION_MAX_LEN, a buffer
+    outside [0, lim) and, with `pages` (batch_dev), a page of the span that
+    holds no buffer byte -- the pairwise rule of the kernel, addresses
+    A(x) = base + x."""
+    M = (1 << 64) - 1
+    n = len(offs)
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        e = (o + L) & M
+        if e < o or L > REGION_MAX_LEN or o > lim or L > lim - o:
+            return True
+        if i + 1 < n:
+            o1, L1 = int(offs[i + 1]), int(lens[i + 1])
+            if e > o1:
+                return True
+            if pages:
+                nz = L1 != 0
+                pn = ((base + o1 - (0 if nz else 1)) & M) >> 12
+                pe = ((base + e - 1) & M) >> 12
+                if pn > pe + (1 if nz else 0):
+                    return True
+        if pages and i == 0 and L == 0:
+            return True
+    return False
+
+
+def route_region_ok(offs, lens, lim: int, base: int, dyn: bool, cap_chunks: int) -> bool:
+    """route_region: not bad, some bytes, and (dyn) the gap rule and the
+    workspace's chunk cap over the span [offsets[0], end of the last)."""
+    if route_plan_bad(offs, lens, lim, base, dyn):
+        return False
+    total = sum(min(int(x), REGION_MAX_LEN + 1) for x in lens)
+    if total == 0:
+        return False
+    if not dyn:
+        return True
+    lo, hi = int(offs[0]), int(offs[-1]) + int(lens[-1])
+    if hi - lo - total > total // 8 + 65536:
+        return False
+    O = (base + lo) & ~4095
+    return (base + hi - O + 4095) // 4096 <= cap_chunks
+
+
+def span_pages_touched(offs, lens, base: int) -> bool:
+    """Every 4 KiB page of the span [A(offsets[0]), A(end of the last)) holds
+    a byte of some non-empty buffer (brute force)."""
+    lo, hi = base + int(offs[0]), base + int(offs[-1]) + int(lens[-1])
+    if hi <= lo:
+        return True
+    touched = set()
+    for o, L in zip(offs, lens):
+        if L:
+            touched.update(range((base + int(o)) >> 12, ((base + int(o) + int(L) - 1) >> 12) + 1))
+    return all(p in touched for p in range(lo >> 12, ((hi - 1) >> 12) + 1))

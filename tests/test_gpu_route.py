@@ -198,3 +198,91 @@ def test_zero_length_and_single(dev, C, port):
     buf = torch.from_numpy(host).to(dev)
     for offs, lens in (([0, 0, 5, 5], [0, 0, 0, 0]), ([100], [0]), ([4095], [1]), ([0], [8192])):
         _both(C, dev, port, host, buf, np.array(offs), np.array(lens), 0)
+
+
+def test_page_rule_boundary(dev, C, port):
+    """batch_dev's page rule (crc32c_route_plan `pages`) around its boundary:
+    the next buffer starting one page past the previous one's last page or
+    inside the page after it (offsets from a tensor whose address is only
+    512-B aligned, so the cases fall on both sides of the rule).  Both routes
+    right, in mapped memory."""
+    for lead, nxt in ((0, 8192), (0, 8191), (4092, 4100), (4092, 4000), (5, 4096 + 4091)):
+        lens = np.array([4096 - lead % 4096 if lead else 4096, 9000, 3000])
+        offs = np.array([lead, lead + nxt, lead + nxt + 9000 + 2])
+        host = port.fill(0x9A6 + nxt, 0, int(offs[-1] + lens[-1]) + 64)
+        _both(C, dev, port, host, torch.from_numpy(host).to(dev), offs, lens, nxt)
+
+
+def test_unmapped_page_between_buffers(dev, C, port):
+    """Two device mappings with an unmapped hole between them (HIP virtual
+    memory: one address reservation, two physical allocations mapped around a
+    hole of one granule) and a sorted batch of 128 KiB buffers on both sides,
+    by absolute address: the hole is small against the bytes (the gap rule
+    alone would take the region path, which reads every page of the span and
+    would fault in the hole); the page rule sends it to the batch path, which
+    reads only the buffers.  Skipped where the virtual memory API is missing."""
+    import ctypes as ct
+    from nvlevelz_amd import _lib  # noqa: F401  (loads the HIP runtime the engine links)
+    hip = ct.CDLL("libamdhip64.so.7")
+
+    class Loc(ct.Structure):
+        _fields_ = [("type", ct.c_int), ("id", ct.c_int)]
+
+    class Flags(ct.Structure):
+        _fields_ = [("compressionType", ct.c_ubyte), ("gpuDirectRDMACapable", ct.c_ubyte), ("usage", ct.c_ushort)]
+
+    class Prop(ct.Structure):
+        _fields_ = [("type", ct.c_int), ("requestedHandleType", ct.c_int), ("location", Loc),
+                    ("win32HandleMetaData", ct.c_void_p), ("allocFlags", Flags)]
+
+    class Access(ct.Structure):
+        _fields_ = [("location", Loc), ("flags", ct.c_int)]
+
+    for f in ("hipMemGetAllocationGranularity", "hipMemAddressReserve", "hipMemCreate", "hipMemMap",
+              "hipMemSetAccess", "hipMemUnmap", "hipMemRelease", "hipMemAddressFree", "hipMemcpy"):
+        getattr(hip, f).restype = ct.c_int
+    torch.cuda.synchronize(dev)
+    prop = Prop(1, 0, Loc(1, dev.index or 0), None, Flags(0, 0, 0))
+    gran = ct.c_size_t(0)
+    if hip.hipMemGetAllocationGranularity(ct.byref(gran), ct.byref(prop), 0) != 0 or gran.value == 0:
+        pytest.skip("hipMemGetAllocationGranularity unavailable")
+    H = gran.value                                   # the hole: one granule
+    D = -(-(24 << 20) // H) * H                      # each mapping
+    va = ct.c_void_p(0)
+    assert hip.hipMemAddressReserve(ct.byref(va), ct.c_size_t(2 * D + H), ct.c_size_t(0), None, ct.c_ulonglong(0)) == 0
+    handles, mapped = [], []
+    try:
+        for k in range(2):
+            h = ct.c_void_p(0)
+            if hip.hipMemCreate(ct.byref(h), ct.c_size_t(D), ct.byref(prop), ct.c_ulonglong(0)) != 0:
+                pytest.skip("hipMemCreate unavailable")
+            handles.append(h)
+            at = va.value + k * (D + H)
+            assert hip.hipMemMap(ct.c_void_p(at), ct.c_size_t(D), ct.c_size_t(0), h, ct.c_ulonglong(0)) == 0
+            mapped.append(at)
+            acc = Access(Loc(1, dev.index or 0), 3)
+            assert hip.hipMemSetAccess(ct.c_void_p(at), ct.c_size_t(D), ct.byref(acc), ct.c_size_t(1)) == 0
+        img = port.fill(0x401E, 0, 2 * D + H)
+        for at in mapped:
+            rel = at - va.value
+            assert hip.hipMemcpy(ct.c_void_p(at), img[rel:rel + D].ctypes.data_as(ct.c_void_p), ct.c_size_t(D), 1) == 0
+        L = 128 << 10
+        k1 = D // L
+        rel = np.concatenate([np.arange(k1) * L, D + H + np.arange(k1) * L]).astype(np.int64)
+        lens = np.full(rel.size, L)
+        assert (rel[k1] - (rel[k1 - 1] + L)) <= lens.sum() // 8 + 65536  # the gap rule would pass
+        want = port.varlen(img, rel.astype(np.uint64), lens.astype(np.uint64))
+        ta, tl = _t64((va.value + rel).astype(np.uint64), dev), _t64(lens, dev)
+        out = torch.empty(rel.size, dtype=torch.int32, device=dev)
+        rc = _lib.lib.nvl_crc32c_batch_dev(None, ta.data_ptr(), tl.data_ptr(), None, 0, out.data_ptr(), rel.size, 0,
+                                           None, 0, torch.cuda.current_stream(dev).cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(_u32(out), want)
+    finally:
+        torch.cuda.synchronize(dev)
+        for at in mapped:
+            hip.hipMemUnmap(ct.c_void_p(at), ct.c_size_t(D))
+        for h in handles:
+            hip.hipMemRelease(h)
+        hip.hipMemAddressFree(va, ct.c_size_t(2 * D + H))

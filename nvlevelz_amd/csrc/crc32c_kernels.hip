@@ -302,7 +302,7 @@ struct RoutePart {
   uint64_t sum;  // sum of the slice's lengths, each capped at kRegionMaxLen + 1 (< 2^43 for n < 2^31)
   uint64_t bad;  // 1: a pair out of order / overlapping, a buffer outside the region or longer than kRegionMaxLen
 };
-constexpr uint32_t kRoutePlanMax = 64;  // plan workgroups (one wave reduces their partials)
+constexpr uint32_t kRoutePlanMax = 128;  // plan workgroups (a wave reduces their partials, two per lane)
 struct Route {
   const RoutePart* parts = nullptr;  // nullptr: no route (the launch is what it is)
   uint32_t np = 0;
@@ -373,15 +373,26 @@ __device__ __forceinline__ uint64_t wave_total_u64(uint64_t v) {
 // lo / hi: the span (dyn).
 __device__ __forceinline__ bool route_region(const Route& r, uint64_t& lo, uint64_t& hi) {
   const int lane = (int)(threadIdx.x & 63u);
-  const uint32_t k = min((uint32_t)lane, r.np - 1u);  // (clamped: every load issued)
-  const RoutePart q = r.parts[k];
+  // lane k takes partials k, k + 64, ... (np <= kRoutePlanMax; the loads together, clamped)
+  RoutePart q[kRoutePlanMax / 64u];
+#pragma unroll
+  for (uint32_t m = 0; m < kRoutePlanMax / 64u; ++m)
+    if (m == 0u || 64u * m < r.np) q[m] = r.parts[min(64u * m + (uint32_t)lane, r.np - 1u)];
   lo = ldc(r.offsets, 0);
   hi = ldc(r.offsets, r.n - 1u) + ldc(r.lengths, r.n - 1u);
-  const bool mine = (uint32_t)lane < r.np;
-  if (__ballot(mine && q.bad != 0u)) return false;
-  if (!__ballot(mine && q.sum != 0u)) return false;  // nothing to checksum
+  bool bad = false, some = false;
+  uint64_t lsum = 0;
+#pragma unroll
+  for (uint32_t m = 0; m < kRoutePlanMax / 64u; ++m) {
+    const bool mine = 64u * m + (uint32_t)lane < r.np;
+    bad |= mine && q[m].bad != 0u;
+    some |= mine && q[m].sum != 0u;
+    lsum += mine ? q[m].sum : 0u;
+  }
+  if (__ballot(bad)) return false;
+  if (!__ballot(some)) return false;  // nothing to checksum
   if (!r.dyn) return true;
-  const uint64_t sum = wave_total_u64(mine ? q.sum : 0u);
+  const uint64_t sum = wave_total_u64(lsum);
   // sorted and non-overlapping: hi - lo >= sum; gaps at most 1/8 of the bytes (+64 KiB)
   if (hi - lo - sum > sum / 8u + 65536u) return false;
   const uintptr_t O = ((uintptr_t)r.base + lo) & ~(uintptr_t)(kChunk - 1u);
@@ -3704,7 +3715,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g
 // byte's page ends (page(A(o) - 1) <= page(A(e_prev) - 1)), and the first
 // buffer is not empty -- so the last byte's page of every prefix is touched
 // and no page is skipped.
-constexpr uint32_t kPlanT = 1024, kPlanPer = 4;
+constexpr uint32_t kPlanT = 512, kPlanPer = 2;  // (shapes A/B'd: tools/diag/abl_plan.sh)
 __global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __restrict__ off,
                                                            const uint64_t* __restrict__ len, uint64_t n, uint64_t lim,
                                                            uintptr_t base, uint32_t pages,
@@ -4118,9 +4129,14 @@ size_t route_parts_bytes() { return (dev::kRoutePlanMax * sizeof(dev::RoutePart)
 // <= kRegionMaxLen (32 chunks), gaps <= 1/8 of the bytes + 64 KiB -> at most
 // 36 chunks per buffer + 18 + 2 (route_verdict checks it).
 uint64_t route_cap_chunks(uint64_t n) { return 36u * n + 20u; }
-static inline uint32_t route_plan_grid(uint64_t n) {  // one step of 4096 pairs per workgroup up to 64 of them
+// Plan workgroups: one step of kPlanT x kPlanPer = 1024 pairs each, but at
+// least ~64 of them from 16K pairs on (the scan is latency-bound: spreading
+// it over more CUs shortens it -- config 3's 32 672 pairs 175.2 -> 173.3 us
+// on 64 workgroups instead of 8, v / r 1.5 us on 98 instead of 25).
+static inline uint32_t route_plan_grid(uint64_t n) {
   const uint64_t per = (uint64_t)dev::kPlanT * dev::kPlanPer;
-  return (uint32_t)std::min<uint64_t>(dev::kRoutePlanMax, std::max<uint64_t>(1, (n + per - 1u) / per));
+  const uint64_t want = std::max<uint64_t>(std::min<uint64_t>(64, (n + 255u) / 256u), (n + per - 1u) / per);
+  return (uint32_t)std::min<uint64_t>(dev::kRoutePlanMax, std::max<uint64_t>(1, want));
 }
 
 hipError_t launch_routed(const LaunchCtx& lc, const uint8_t* base, uint64_t region_len, bool dyn,

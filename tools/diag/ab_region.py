@@ -35,7 +35,7 @@ buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
 libs[0].nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, 0x5EED00B1, None)
 o = torch.from_numpy(offs).to(dev); m = torch.from_numpy(lens).to(dev)
 outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
-wsb = libs[0].nvl_crc32c_region_workspace_bytes(total, n)
+wsb = max(lib.nvl_crc32c_region_workspace_bytes(total, n) for lib in libs)  # (variants may need more)
 ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
 st = torch.cuda.current_stream().cuda_stream
 # NVL_CRC32C_FLAG_REGION_SHAPED by default: the region kernel alone (AB_FLAGS=0: the routed call)
@@ -56,7 +56,9 @@ rounds, reps = int(os.environ.get("AB_ROUNDS", "10")), int(os.environ.get("AB_RE
 per = [[] for _ in range(len(libs) + 1)]
 single = [[] for _ in range(len(libs) + 1)]
 for k in range(len(libs) + 1):
-    for _ in range(5): run(k)
+    for _ in range(5):
+        rc = run(k)
+        assert rc == 0, (k, rc)
 torch.cuda.synchronize()
 import time
 t0 = time.perf_counter()  # ~100 ms of load first: the GPU's sustained-load state (the first ~30 ms run slower)

@@ -286,3 +286,24 @@ def test_unmapped_page_between_buffers(dev, C, port):
         for h in handles:
             hip.hipMemRelease(h)
         hip.hipMemAddressFree(va, ct.c_size_t(2 * D + H))
+
+
+def test_partials_past_the_first_64(dev, C, port):
+    """10^5 buffers: the plan runs ~98 workgroups, so the verdict reads
+    partials beyond lane 63's first (two per lane).  A single pair out of
+    order near the end -- in a partial past the 64th -- must send the batch
+    to the batch path on both entries; the same batch sorted takes the region
+    path.  Every CRC against the oracle."""
+    rng = np.random.default_rng(100)
+    n = 100_000
+    lens = rng.integers(1000, 1200, n)
+    offs = _packed(lens, 3, lead=5)
+    host = port.fill(0x1E5, 0, int(offs[-1] + lens[-1]) + 64)
+    buf = torch.from_numpy(host).to(dev)
+    _both(C, dev, port, host, buf, offs, lens, 1)
+    swapped = offs.copy()
+    j = n - 7
+    swapped[[j, j + 1]] = swapped[[j + 1, j]]
+    lsw = lens.copy()
+    lsw[[j, j + 1]] = lsw[[j + 1, j]]
+    _both(C, dev, port, host, buf, swapped, lsw, 2)

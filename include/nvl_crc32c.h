@@ -154,8 +154,8 @@ NVL_API size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, u
  * most NVL_CRC32C_REGION_MAX_LEN bytes, the first one not empty, no 4 KiB
  * page between the first and the last byte without a buffer byte (only the
  * buffers' own pages are read: buffers from different allocations are safe),
- * gaps between buffers at most 1/8 of the buffer bytes + 64 KiB -- is
- * checksummed over its own span by the region path (see
+ * gaps between buffers at most 1/8 of the buffer bytes + 64 KiB, a span of
+ * at most 64 GiB -- is checksummed over its own span by the region path (see
  * nvl_crc32c_region_dev), any other by the batch kernels. */
 NVL_API int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64_t* lengths,
                          const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,

@@ -4128,7 +4128,10 @@ size_t route_parts_bytes() { return (dev::kRoutePlanMax * sizeof(dev::RoutePart)
 // Region chunks a region-shaped batch_dev batch can span: sorted, each buffer
 // <= kRegionMaxLen (32 chunks), gaps <= 1/8 of the bytes + 64 KiB -> at most
 // 36 chunks per buffer + 18 + 2 (route_verdict checks it).
-uint64_t route_cap_chunks(uint64_t n) { return 36u * n + 20u; }
+// Capped at 2^24 chunks (64 MiB of raws, a 64 GiB span): a larger batch
+// takes the batch path rather than a workspace of 4 bytes per 4 KiB of the
+// worst case (10^7 buffers would have reserved 1.4 GB).
+uint64_t route_cap_chunks(uint64_t n) { return std::min<uint64_t>(36u * n + 20u, 1ull << 24); }
 // Plan workgroups: one step of kPlanT x kPlanPer = 1024 pairs each, but at
 // least ~64 of them from 16K pairs on (the scan is latency-bound: spreading
 // it over more CUs shortens it -- config 3's 32 672 pairs 175.2 -> 173.3 us

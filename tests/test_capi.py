@@ -146,3 +146,16 @@ int main() {
     subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", inc, str(src), "-L", lib, "-lnvl_crc32c",
                     f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
     subprocess.run([str(exe)], check=True)
+
+
+def test_routed_workspace_is_bounded(L):
+    """nvl_crc32c_batch_workspace_bytes covers the routed call's region part
+    (4 bytes per 4 KiB chunk of the largest region-shaped span, 32 bytes of
+    event records per buffer), the chunk part capped at 2^24 chunks (a 64
+    GiB span): 10^7 buffers need well under a gigabyte, not the 1.4 GB of
+    raws an uncapped 36 chunks per buffer would reserve."""
+    small = L.lib.nvl_crc32c_batch_workspace_bytes(100_000)
+    assert 14_400_000 < small < 40_000_000
+    big = L.lib.nvl_crc32c_batch_workspace_bytes(10_000_000)
+    assert big < 700_000_000
+    assert big - 32 * 10_000_000 >= 4 * (1 << 24)

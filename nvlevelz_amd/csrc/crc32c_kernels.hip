@@ -377,7 +377,7 @@ __device__ __forceinline__ bool route_region(const Route& r, uint64_t& lo, uint6
   RoutePart q[kRoutePlanMax / 64u];
 #pragma unroll
   for (uint32_t m = 0; m < kRoutePlanMax / 64u; ++m)
-    if (m == 0u || 64u * m < r.np) q[m] = r.parts[min(64u * m + (uint32_t)lane, r.np - 1u)];
+    q[m] = (m == 0u || 64u * m < r.np) ? r.parts[min(64u * m + (uint32_t)lane, r.np - 1u)] : RoutePart{0u, 0u};
   lo = ldc(r.offsets, 0);
   hi = ldc(r.offsets, r.n - 1u) + ldc(r.lengths, r.n - 1u);
   bool bad = false, some = false;

@@ -1,7 +1,9 @@
 """Phase timeline of the head kernel (run_heads) on a variable-length batch,
 from a diagnostic variant build with tools/diag/stamps.h force-included:
     make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h"
-    CFG=r|v|3 LIB=build/libnvl_crc32c_stamps.so python tools/diag/tl.py
+    CFG=r|v|3|u LIB=build/libnvl_crc32c_stamps.so python tools/diag/tl.py
+(r, v, 3 are region-shaped and batch_dev now routes them to the region path;
+u -- shuffled aligned 4 KiB -- keeps the head kernel's work, in the route kernel)
 Stamps per wave (s_memrealtime, 100 MHz): 0 entry, 1 after the tile scan,
 2 tables in LDS, 3 rounds done (last sub-range), 4 list barrier passed,
 5 long-head drain done, 7 exit.  Prints percentiles of each phase (us) and
@@ -22,12 +24,16 @@ if cfg == "3":
     import oracle
     lens = oracle.port().cfg3_lengths(0x5EED0003, 1 << 30).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+elif cfg == "u":  # 10^5 aligned 4 KiB buffers in random order: not region-shaped, the route kernel runs the heads
+    n = 100_000
+    lens = np.full(n, 4096, dtype=np.int64)
+    offs = np.random.default_rng(3).permutation(n).astype(np.int64) * 4096
 else:
     n = 100_000
     lens = np.full(n, 4097, dtype=np.int64) if cfg == "v" else np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
 n = lens.size
-total = int(offs[-1] + lens[-1]) + 64
+total = int((offs + lens).max()) + 64
 buf = torch.empty(total, dtype=torch.uint8, device=dev)
 lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), total // 8, 8, 0, 1, 0x5EED00B1, None)
 o = torch.from_numpy(offs).to(dev); m = torch.from_numpy(lens).to(dev)

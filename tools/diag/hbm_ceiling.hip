@@ -1,0 +1,89 @@
+// The measured read-only ceiling SURVEY.md §8d asks for beside the 8 TB/s
+// spec: plain streaming kernels that only read a 410 MB buffer (config 2's
+// bytes) and XOR-reduce it, in several launch shapes and load forms; per
+// shape the sustained period over 200 back-to-back launches after warm-up
+// (HIP events), in us and TB/s.  Build: hipcc -O3 --offload-arch=gfx950
+// tools/diag/hbm_ceiling.hip -o tools/diag/hbm_ceiling
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// grid-stride, UNROLL independent 16-byte loads per thread per step
+template <int UNROLL, bool NT>
+__global__ void stream_k(const u32x4* __restrict__ p, uint64_t n16, uint32_t* out) {
+  uint32_t x = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) v[k] = NT ? __builtin_nontemporal_load(p + i + k * stride) : p[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  for (; i < n16; i += stride) {
+    const u32x4 v = p[i];
+    x ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+
+// contiguous 4 KiB blocks per workgroup (the engine's access shape): block b
+// of 64 lanes x 16 B x 4 rows, workgroups take blocks b, b + G, ...
+template <bool NT>
+__global__ void blocks_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint32_t* out) {
+  uint32_t x = 0;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (uint64_t b = (uint64_t)blockIdx.x * nw + wv; b < nblocks; b += (uint64_t)gridDim.x * nw) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(p + b * 4096u);
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = NT ? __builtin_nontemporal_load(q + 64 * j + lane) : q[64 * j + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+
+template <class F>
+static float period(F launch, int R = 200) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int i = 0; i < 100; ++i) launch();
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(a);
+  for (int i = 0; i < R; ++i) launch();
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms * 1000.0f / R;
+}
+
+int main() {
+  const uint64_t bytes = 410000000ull / 4096 * 4096;  // 100096 KiB-blocks ~ config 2's 4.1e8 B
+  uint8_t* p;
+  uint32_t* out;
+  if (hipMalloc(&p, bytes) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
+  (void)hipMemset(p, 0x5a, bytes);
+  const uint64_t n16 = bytes / 16, nblk = bytes / 4096;
+  auto rep = [&](const char* what, float us) {
+    printf("{\"shape\": \"%s\", \"bytes\": %llu, \"period_us\": %.2f, \"TB_s\": %.3f, \"frac_of_8TBs\": %.4f}\n", what,
+           (unsigned long long)bytes, us, bytes / (us * 1e-6) / 1e12, bytes / (us * 1e-6) / 8e12);
+  };
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  for (int pass = 0; pass < 2; ++pass) {
+    rep("grid-stride 256 x 1024, 1 x 16 B nt", period([&] { hipLaunchKernelGGL((stream_k<1, true>), dim3(256), dim3(1024), 0, 0, q, n16, out); }));
+    rep("grid-stride 256 x 1024, 4 x 16 B nt", period([&] { hipLaunchKernelGGL((stream_k<4, true>), dim3(256), dim3(1024), 0, 0, q, n16, out); }));
+    rep("grid-stride 256 x 1024, 4 x 16 B", period([&] { hipLaunchKernelGGL((stream_k<4, false>), dim3(256), dim3(1024), 0, 0, q, n16, out); }));
+    rep("grid-stride 1024 x 256, 4 x 16 B nt", period([&] { hipLaunchKernelGGL((stream_k<4, true>), dim3(1024), dim3(256), 0, 0, q, n16, out); }));
+    rep("grid-stride 2048 x 512, 2 x 16 B nt", period([&] { hipLaunchKernelGGL((stream_k<2, true>), dim3(2048), dim3(512), 0, 0, q, n16, out); }));
+    rep("4 KiB blocks per wave, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocks_k<true>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
+    rep("4 KiB blocks per wave, 256 x 1024", period([&] { hipLaunchKernelGGL((blocks_k<false>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
+    rep("4 KiB blocks per wave, 2048 x 256 nt", period([&] { hipLaunchKernelGGL((blocks_k<true>), dim3(2048), dim3(256), 0, 0, p, nblk, out); }));
+  }
+  return 0;
+}

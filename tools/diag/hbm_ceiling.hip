@@ -47,6 +47,29 @@ __global__ void blocks_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint32
   if (x == 0x12345678u) out[0] = x;
 }
 
+// D 4-KiB blocks per wave per step, loaded together (bytes in flight per
+// wave = D x 4 KiB), at the engine's occupancy (256 x 1024)
+template <int D>
+__global__ void blocksD_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint32_t* out) {
+  uint32_t x = 0;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t W = (uint64_t)gridDim.x * nw;
+  for (uint64_t b = ((uint64_t)blockIdx.x * nw + wv) * D; b < nblocks; b += W * D) {
+    u32x4 v[D][4];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const u32x4* q = reinterpret_cast<const u32x4*>(p + min(b + d, nblocks - 1) * 4096u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[d][j] = __builtin_nontemporal_load(q + 64 * j + lane);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x ^= v[d][j].x ^ v[d][j].y ^ v[d][j].z ^ v[d][j].w;
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+
 template <class F>
 static float period(F launch, int R = 200) {
   hipEvent_t a, b;
@@ -84,6 +107,9 @@ int main() {
     rep("4 KiB blocks per wave, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocks_k<true>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
     rep("4 KiB blocks per wave, 256 x 1024", period([&] { hipLaunchKernelGGL((blocks_k<false>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
     rep("4 KiB blocks per wave, 2048 x 256 nt", period([&] { hipLaunchKernelGGL((blocks_k<true>), dim3(2048), dim3(256), 0, 0, p, nblk, out); }));
+    rep("2 x 4 KiB blocks per wave per step, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocksD_k<2>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
+    rep("3 x 4 KiB blocks per wave per step, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocksD_k<3>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
+    rep("4 x 4 KiB blocks per wave per step, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocksD_k<4>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
   }
   return 0;
 }

@@ -273,7 +273,6 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   void* tmp = w + L.tmp;
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   const bool small = var_plan_small(n);
-#if !defined(NVL_NO_FUSED)
   if (s->num_cu <= 1023) lc.counter = counters_for(s, st);
   if (lc.counter) {  // (cs holds lpre, the unit map region the tiles)
     hipError_t ef =
@@ -284,7 +283,6 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
     if (own) (void)hipFreeAsync(ws, st);
     return hip_rc(ef);
   }
-#endif
   hipError_t e;
   if (small) {
     e = launch_var_plan_small(lc, lengths, n, cs, unit_first, long_bufs);

@@ -1181,17 +1181,13 @@ __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* 
 // boundary leaves a head/tail record for crc32c_fixup_kernel.  The next
 // chunk -- including the first chunk of the next unit -- is always in flight
 // while the current one computes.
-#ifndef NVL_UNIT_STEP
-#define NVL_UNIT_STEP 1  // chunks per step in scheduler B (2: interleaved pair; A/B'd, no gain)
-#endif
-#ifndef NVL_UNIT_STEP_ALIGNED
-#define NVL_UNIT_STEP_ALIGNED 2  // the same for the aligned (kAligned, J > 1) kernel: no spills there (cfg4 -3 %)
-#endif
+constexpr int kUnitStep = 1;         // chunks per step in scheduler B (2: interleaved pair; A/B'd, no gain)
+constexpr int kUnitStepAligned = 2;  // the same for the aligned (kAligned, J > 1) kernel: no spills there (cfg4 -3 %)
 
 template <int M, int NW, class G>
 __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* lds) {
   NVL_STAMP0();
-  constexpr int kStep = M == kAligned ? NVL_UNIT_STEP_ALIGNED : NVL_UNIT_STEP;
+  constexpr int kStep = M == kAligned ? kUnitStepAligned : kUnitStep;
   static_assert(M == kAligned || kStep == 1, "the kGeneral loop skips head chunks one step at a time");
   const int lane = threadIdx.x & 63;
   const uint32_t wv = uniform_u32(threadIdx.x >> 6);
@@ -1388,13 +1384,9 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   const int lane = threadIdx.x & 63;
   const uint32_t wv = uniform_u32(threadIdx.x >> 6);
   const uint64_t nb = i1 > i0 ? i1 - i0 : 0;
-#ifndef NVL_BUFS_DIV
-#define NVL_BUFS_DIV 4  // about this many GS-buffer groups per wave
-#endif
-  const uint32_t GS = (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (NVL_BUFS_DIV * NW)));  // buffers per group
-#ifndef NVL_BUFS_TAIL
-#define NVL_BUFS_TAIL 0  // single-buffer groups for the range's last buffers (tuning knob)
-#endif
+constexpr int kBufsDiv = 4;  // about this many GS-buffer groups per wave
+  const uint32_t GS = (uint32_t)max<uint64_t>(1, min<uint64_t>(kWave, nb / (kBufsDiv * NW)));  // buffers per group
+constexpr int kBufsTail = 0;  // single-buffer groups for the range's last buffers (A/B'd: none)
   // Groups of GS buffers (optionally single-buffer groups for the range's
   // last kBT buffers).  The singles once evened out the waves' ends (12 us
   // apart on 10^5 x 4097 B, 27 us on config 3); with the buffers handed out
@@ -1402,7 +1394,7 @@ __device__ __forceinline__ void run_bufs(const G& g, const KArgs& ka, uint8_t* l
   // they only cost single-chunk steps: 64 -> 0 took 10^5 x 4097 B from 101
   // to 91 us per call and 10^5 x 3364..4109 B from 124 to 115 us, config 3
   // unchanged within the box's spread (tools/diag/ab_variants.sh, same box).
-  const uint64_t kBT = NVL_BUFS_TAIL;
+  const uint64_t kBT = kBufsTail;
   const uint64_t nbig = nb > kBT * 2 ? (nb - kBT) / GS : 0;  // GS-buffer groups
   const uint64_t ngroups = nbig + (nb - nbig * GS);
   const uintptr_t safe = (uintptr_t)ka.tables;
@@ -2252,48 +2244,35 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_head_kernel(G g, KArgs ka)
   run_heads(g, ka, lds);
 }
 
-#ifndef NVL_FAST_U
-#define NVL_FAST_U 2  // buffers per unit in scheduler A (tools/ab_bench.py: 2 > 1 > 4)
-#endif
+constexpr int kFastU = 2;  // buffers per unit in scheduler A (tools/ab_bench.py: 2 > 1 > 4)
 
-#ifndef NVL_GEN_WAVES
-#define NVL_GEN_WAVES 16  // waves per workgroup of the kGeneral kernels
-#endif
-constexpr int kGenWaves = NVL_GEN_WAVES;
+constexpr int kGenWaves = 16;  // waves per workgroup of the kGeneral kernels
 template <int M>
 constexpr int waves_of() { return M == kGeneral ? kGenWaves : kWavesPerWG; }
 
 template <int M>
-#ifndef NVL_FIXED_NIB
-#define NVL_FIXED_NIB 1  // 1: config 2's chunks fold through the nibble lane shifts (chains<NIB>)
-#endif
 __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes > kRLdsBytes ? kLdsBytes : kRLdsBytes];
   if constexpr (M == kAligned) {
     if (g.J == 1) {
-      run_pairs<NVL_FAST_U, kWavesPerWG, kAligned, FixedGeom, false, NVL_FIXED_NIB != 0>(g, ka, lds);
+      run_pairs<kFastU, kWavesPerWG, kAligned, FixedGeom, false, true>(g, ka, lds);
       return;
     }
   }
-#ifndef NVL_GEN_PAIR_U
-#define NVL_GEN_PAIR_U 2  // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 91.7 through run_units)
-#endif
+constexpr int kGenPairU = 2;  // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 91.7 through run_units)
   if constexpr (M == kGeneral) {
-#if !defined(NVL_GEN_NO_PAIRS)
     // one whole chunk per buffer (len == 4096, any alignment): scheduler A,
     // one buffer per unit, no records
     if (g.J == 1 && !head_first(g.len)) {
-      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
+      run_pairs<kGenPairU, waves_of<M>(), kGeneral>(g, ka, lds);
       return;
     }
-#endif
     // one partial chunk per buffer, 1025..4095 bytes (launch_fixed): each
     // buffer a long head, in scheduler A's order (10^5 x 3500 B at stride
     // 4128: 75.3 -> 71.3 us against the head kernel, profiles/r03_ablations).
-    // Outside the variant switch above: launch_fixed sends these batches here
-    // without a head kernel, so no build may drop this path.
+    // (launch_fixed sends these batches here without a head kernel.)
     if (g.J == 1) {
-      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kMasked>(g, ka, lds);
+      run_pairs<kGenPairU, waves_of<M>(), kMasked>(g, ka, lds);
       return;
     }
   }
@@ -2305,7 +2284,7 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
 // independent scheduler-A pass (ChunkGeom), raw registers to KArgs::raws.
 __global__ __launch_bounds__(kThreads, 1) void crc32c_chunks_kernel(ChunkGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes > kRLdsBytes ? kLdsBytes : kRLdsBytes];
-  run_pairs<NVL_FAST_U, kWavesPerWG, kAligned, ChunkGeom, true, NVL_FIXED_NIB != 0>(g, ka, lds);
+  run_pairs<kFastU, kWavesPerWG, kAligned, ChunkGeom, true, true>(g, ka, lds);
 }
 
 // Buffer i of J chunks: raw = XOR_c shift(raws[iJ + c], 4096 (J - 1 - c)).
@@ -2398,12 +2377,9 @@ __global__ __launch_bounds__(256) void crc32c_fold_seg_kernel(FoldSeg a) {
   }
 }
 
-#ifndef NVL_VAR_BUFS
-#define NVL_VAR_BUFS 1  // 1: scheduler C when every buffer has <= kBufsMaxJ chunks
-#endif
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_kernel(VarGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-  if (NVL_VAR_BUFS && ka.long_bufs && ldc(ka.long_bufs, 0) == 0u) {
+  if (ka.long_bufs && ldc(ka.long_bufs, 0) == 0u) {
     // Workgroup b: the buffers that start in its chunk range [lo(64b),
     // lo(64b+64)): unit_first[u] holds the buffer containing chunk lo(u),
     // which starts there or earlier (then it is the previous workgroup's).
@@ -2854,7 +2830,7 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   const uint32_t* ubuf = reinterpret_cast<const uint32_t*>(lds + kUnitOff);
   const VarGeomFused g{gv.base, gv.offsets, gv.lengths, gv.n, gv.init, gv.init_all, C0, C1, ubuf,
                        ubuf + kUnitsPerWG, ub0};
-  if (NVL_VAR_BUFS && !long_bufs) {
+  if (!long_bufs) {
     // whole buffers: no records, so no edge fold either -- no grid-wide
     // hand-off (its sc1 stores, drain and counter round trip cost ~5 us of
     // tail; the stream's counter is left untouched, i.e. zero)
@@ -3684,7 +3660,7 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
 
 __global__ __launch_bounds__(kThreads, 1) void crc32c_region_kernel(RegionGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRLdsBytes];
-  run_region<NVL_FAST_U>(g, ka, lds, gridDim.x);
+  run_region<kFastU>(g, ka, lds, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -3789,7 +3765,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg
     const uint64_t gw = (rg.nc + kWavesPerWG - 1u) / kWavesPerWG;  // (the host's grid_for)
     const uint32_t G = (uint32_t)max<uint64_t>(1u, min<uint64_t>(gridDim.x, gw));
     if (blockIdx.x >= G) return;
-    run_region<NVL_FAST_U>(rg, ka, lds, G);
+    run_region<kFastU>(rg, ka, lds, G);
   } else {
     if (blockIdx.x >= ka.tile_G) return;
     run_heads(vg, ka, lds);
@@ -3855,12 +3831,10 @@ static inline uint32_t chunks_of(uint64_t len) { return dev::chunks_for(len); }
 
 // The head kernel over a geometry's n buffers; its dispatch records
 // ev_start when given (it is then the call's first kernel).
-#ifndef NVL_HEAD_GRID_MULT
-#define NVL_HEAD_GRID_MULT 1  // head kernel workgroups per CU (tuning knob; the fused plan takes <= 1023 tiles)
-#endif
+constexpr uint32_t kHeadGridMult = 1;  // head kernel workgroups per CU (A/B'd; the fused plan takes <= 1023 tiles)
 static inline uint32_t head_grid(int num_cu, uint64_t n) {
   const uint64_t per_wg = 8u * dev::kWavesPerWG;  // at least ~8 buffers per wave
-  const uint64_t cap = std::min<uint64_t>((uint64_t)num_cu * NVL_HEAD_GRID_MULT, dev::kMaxTiles);
+  const uint64_t cap = std::min<uint64_t>((uint64_t)num_cu * kHeadGridMult, dev::kMaxTiles);
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, (n + per_wg - 1) / per_wg));
 }
 

@@ -21,14 +21,14 @@ rep("""  } else {
 rep("""    realign_general(chunk_end(bi, c), false, (uintptr_t)bi.p, bi.s, lane, ch, w);""",
     """    realign_general(chunk_end(bi, c), M == kMasked, (uintptr_t)bi.p, bi.s, lane, ch, w);""")
 rep("""    if (g.J == 1 && !head_first(g.len)) {
-      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
+      run_pairs<kGenPairU, waves_of<M>(), kGeneral>(g, ka, lds);
       return;
     }""", """    if (g.J == 1 && !head_first(g.len)) {
-      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kGeneral>(g, ka, lds);
+      run_pairs<kGenPairU, waves_of<M>(), kGeneral>(g, ka, lds);
       return;
     }
     if (g.J == 1 && g.len >= 1025) {
-      run_pairs<NVL_GEN_PAIR_U, waves_of<M>(), kMasked>(g, ka, lds);
+      run_pairs<kGenPairU, waves_of<M>(), kMasked>(g, ka, lds);
       return;
     }""")
 rep("""  const bool heads = !aligned && dev::head_first(len);  // every buffer's first chunk is a head chunk""",

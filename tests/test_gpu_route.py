@@ -307,3 +307,23 @@ def test_partials_past_the_first_64(dev, C, port):
     lsw = lens.copy()
     lsw[[j, j + 1]] = lsw[[j + 1, j]]
     _both(C, dev, port, host, buf, swapped, lsw, 2)
+
+
+def test_million_small_buffers(dev, C, port):
+    """10^6 packed buffers of 1..200 bytes through both entries: the plan's
+    128 workgroups each loop over ~7800 pairs (several steps), the region
+    path folds ~3900 buffers per workgroup; the same batch with one pair
+    swapped in the middle takes the batch path.  Every CRC against the
+    oracle."""
+    rng = np.random.default_rng(10 ** 6)
+    n = 1_000_000
+    lens = rng.integers(1, 201, n)
+    offs = _packed(lens, 0, lead=3)
+    host = port.fill(0x1E6, 0, int(offs[-1] + lens[-1]) + 64)
+    buf = torch.from_numpy(host).to(dev)
+    _both(C, dev, port, host, buf, offs, lens, 3)
+    j = n // 2
+    offs2, lens2 = offs.copy(), lens.copy()
+    offs2[[j, j + 1]] = offs2[[j + 1, j]]
+    lens2[[j, j + 1]] = lens2[[j + 1, j]]
+    _both(C, dev, port, host, buf, offs2, lens2, 4)

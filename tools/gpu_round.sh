@@ -12,6 +12,8 @@
 #   shims   rocprofv3 kernel trace of the whole-table verify shim bench
 #   smoke   __graft_entry__.smoke();  default  python3 bench.py with no flags (the driver's BENCH line)
 #   pmc     tools/pmc.sh (full counter set) on cfg2, rand (3364..4109 B), var4097, cfg3
+#   ceiling tools/diag/hbm_ceiling (read-only streaming kernels: the measured HBM read ceiling;
+#           built here first: hipcc -O3 --offload-arch=gfx950 tools/diag/hbm_ceiling.hip -o tools/diag/hbm_ceiling)
 set -o pipefail
 TAG=${1:-r03}
 shift
@@ -47,6 +49,7 @@ for s in $STEPS; do
       NVL_BENCH_BACKEND=gloo run spawn_cfg2 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-e2e ;;
     configs) run configs 600 python3 tools/bench_configs.py --configs 2,3,3R,3S,4,v,vR,vS,r,rR,rS,g,u,uR,big1 ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    ceiling) run ceiling 120 ./tools/diag/hbm_ceiling ;;
     default) run bench_default 400 python3 bench.py ;;
     pmc)
       for c in cfg2 rand var4097 cfg3; do

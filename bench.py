@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--shims", action="store_true",
                     help="also time the whole-table verify shim on a host-resident 10^5-block SSTable image")
     ap.add_argument("--verify", action="store_true", default=True)
+    ap.add_argument("--probe", type=int, default=200,
+                    help="launches of the read-only probe kernel timed after the timed region (0: skip)")
     ap.add_argument("--sustained", type=int, default=2000,
                     help="untimed back-to-back launches after the timed region (segment periods; 0 = skip)")
     return ap.parse_args()
@@ -604,6 +606,24 @@ def main():
         segs = [sev[j].elapsed_time(sev[j + 1]) * 1e3 / seg for j in range(nseg)]
         sus = {"launches": nseg * seg, "segment_launches": seg,
                "segment_period_us": [round(x, 2) for x in segs]}
+    #  * the measured read ceiling on the same buffer: a plain streaming
+    #    kernel (nvl_crc32c_read_probe) back to back, period by HIP events --
+    #    what this box's HBM gives a read-only kernel in this very run
+    probe = None
+    if args.probe > 0:
+        nb = (buf.numel() // 16) * 16
+        sink = torch.zeros(1, dtype=torch.int32, device=dev)
+        from nvlevelz_amd import _lib as nvl_lib
+        lib = nvl_lib.lib
+        for _ in range(50):
+            assert lib.nvl_crc32c_read_probe(buf.data_ptr(), nb, sink.data_ptr(), stream.cuda_stream) == 0
+        pe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        pe[0].record(stream)
+        for _ in range(args.probe):
+            lib.nvl_crc32c_read_probe(buf.data_ptr(), nb, sink.data_ptr(), stream.cuda_stream)
+        pe[1].record(stream)
+        torch.cuda.synchronize()
+        probe = {"bytes": nb, "period_us": pe[0].elapsed_time(pe[1]) * 1e3 / args.probe}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -720,6 +740,20 @@ def main():
                         "what": "untimed diagnostic after the timed region: back-to-back launches, HIP events every "
                                 "100; frac over the whole run (the timed window's frac is roofline.frac)"})
             line["roofline"]["sustained"] = sus
+        if probe:
+            cg = probe["bytes"] / (probe["period_us"] * 1e-6) / 1e9
+            line["roofline"]["read_ceiling"] = {
+                "period_us": round(probe["period_us"], 2), "achieved": round(cg, 1), "unit": "GB/s",
+                "frac_of_peak": round(cg / HBM_PEAK_GBS, 4), "kernel_over_ceiling": round(achieved / cg, 4),
+                "what": "untimed diagnostic: nvl_crc32c_read_probe (a read-only streaming kernel, four 16-byte "
+                        "nontemporal loads in flight per thread, 256 x 1024) back to back over the same buffer on "
+                        "the same box, %d launches after 50, run after the sustained pass; kernel_over_ceiling = "
+                        "roofline.achieved / this rate (the short timed window, which still ramps); "
+                        "sustained_over_ceiling = the same for roofline.sustained's mean period, both ramped "
+                        "(DESIGN.md section 4)" % args.probe}
+            if sus:
+                line["roofline"]["read_ceiling"]["sustained_over_ceiling"] = round(
+                    alg_bytes / (sus["mean_period_us"] * 1e-6) / 1e9 / cg, 4)
         if c5:
             line["cfg5"] = c5
         if e2e:

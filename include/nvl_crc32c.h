@@ -252,6 +252,15 @@ NVL_API int nvl_crc32c_fill_splitmix(void* dst, uint64_t nblocks, uint64_t block
                                      uint64_t first_block, uint64_t block_step, uint64_t seed,
                                      void* stream);
 
+/* (harness) The measured read ceiling: one launch of a plain streaming
+ * kernel that reads `bytes` (a multiple of 16) at `src` and XOR-reduces them
+ * -- four 16-byte nontemporal loads in flight per thread, grid-strided, 256
+ * workgroups of 1024 threads (the best read-only shape measured on gfx950,
+ * DESIGN.md §4) -- so that a benchmark can time the HBM read rate beside the
+ * engine's kernels in the same run.  Writes 4 bytes at `sink` only when the
+ * XOR of the data is 0x12345678.  Asynchronous on `stream`. */
+NVL_API int nvl_crc32c_read_probe(const void* src, uint64_t bytes, uint32_t* sink, void* stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -55,6 +55,7 @@ SIGNATURES = {
     "nvl_crc32c_batch_host": (_int, [_vp, _vp, _vp, _u32, _vp, _u64, _u32]),
     "nvl_crc32c_fixed_host": (_int, [_vp, _u64, _u64, _u64, _vp, _u32, _vp, _u32]),
     "nvl_crc32c_fill_splitmix": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
+    "nvl_crc32c_read_probe": (_int, [_vp, _u64, _vp, _vp]),
     "nvl_crc32c_batch_region_host": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32]),
     "nvl_crc32c_batch_region_host_multi": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32, _vp, _int, _u64]),
     "nvl_crc32c_multi_plan": (_int, [_vp, _vp, _u64, _int, _u64, _vp]),

@@ -3772,6 +3772,27 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg
   }
 }
 
+// The read ceiling probe (nvl_crc32c_read_probe): grid-strided, four
+// independent 16-byte nontemporal loads per thread per step.
+__global__ __launch_bounds__(1024) void read_probe_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                          uint32_t* __restrict__ sink) {
+  uint32_t x = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3u * stride < n16; i += 4u * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(p + i + (uint64_t)k * stride);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  for (; i < n16; i += stride) {
+    const u32x4 v = p[i];
+    x ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (x == 0x12345678u) sink[0] = x;
+}
+
 // Synthetic stream: one thread per 8-byte word.
 __global__ void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t words_per_block, uint64_t nwords,
                                      uint64_t first_block, uint64_t block_step, uint64_t seed) {
@@ -3807,6 +3828,12 @@ hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64
   const uint64_t blocks = std::min<uint64_t>((nwords + 255) / 256, 65536);
   hipLaunchKernelGGL(dev::fill_splitmix_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
                      static_cast<uint64_t*>(dst), wpb, nwords, first_block, block_step, seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_probe(const void* src, uint64_t bytes, uint32_t* sink, hipStream_t st) {
+  hipLaunchKernelGGL(dev::read_probe_kernel, dim3(256), dim3(1024), 0, st, static_cast<const dev::u32x4*>(src),
+                     bytes / 16u, sink);
   return hipGetLastError();
 }
 

@@ -70,6 +70,46 @@ __global__ void blocksD_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint3
   if (x == 0x12345678u) out[0] = x;
 }
 
+// 4 blocks per wave at a quarter of the batch apart, taken row by row: step
+// j loads row j (1 KiB) of each of the 4 blocks -- 4 KiB per wave in flight,
+// as blocks_k, but from four distant places (the grid-stride streamer's
+// spread) -- a layout a CRC kernel could use (each row is 16 whole pieces).
+__global__ void blocks_spread_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint32_t* out) {
+  uint32_t x = 0;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t Q = nblocks / 4, W = (uint64_t)gridDim.x * nw;
+  for (uint64_t b = (uint64_t)blockIdx.x * nw + wv; b < Q; b += W) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u32x4 v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + (b + (uint64_t)c * Q) * 4096u) + 64 * j + lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x ^= v[c].x ^ v[c].y ^ v[c].z ^ v[c].w;
+    }
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+// the same four blocks adjacent (b, b+1, b+2, b+3), row by row
+__global__ void blocks_rows_adj_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint32_t* out) {
+  uint32_t x = 0;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t W = (uint64_t)gridDim.x * nw;
+  for (uint64_t b = ((uint64_t)blockIdx.x * nw + wv) * 4; b + 3 < nblocks; b += W * 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u32x4 v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + (b + (uint64_t)c) * 4096u) + 64 * j + lane);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x ^= v[c].x ^ v[c].y ^ v[c].z ^ v[c].w;
+    }
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+
 template <class F>
 static float period(F launch, int R = 200) {
   hipEvent_t a, b;
@@ -110,6 +150,8 @@ int main() {
     rep("2 x 4 KiB blocks per wave per step, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocksD_k<2>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
     rep("3 x 4 KiB blocks per wave per step, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocksD_k<3>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
     rep("4 x 4 KiB blocks per wave per step, 256 x 1024 nt", period([&] { hipLaunchKernelGGL((blocksD_k<4>), dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
+    rep("4 distant blocks per wave row by row, 256 x 1024 nt", period([&] { hipLaunchKernelGGL(blocks_spread_k, dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
+    rep("4 adjacent blocks per wave row by row, 256 x 1024 nt", period([&] { hipLaunchKernelGGL(blocks_rows_adj_k, dim3(256), dim3(1024), 0, 0, p, nblk, out); }));
   }
   return 0;
 }

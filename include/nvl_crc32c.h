@@ -253,7 +253,8 @@ NVL_API int nvl_crc32c_fill_splitmix(void* dst, uint64_t nblocks, uint64_t block
                                      void* stream);
 
 /* (harness) The measured read ceiling: one launch of a plain streaming
- * kernel that reads `bytes` (a multiple of 16) at `src` and XOR-reduces them
+ * kernel that reads `bytes` (a multiple of 16) at `src` (16-byte aligned; else
+ * NVL_CRC32C_EINVAL) and XOR-reduces them
  * -- four 16-byte nontemporal loads in flight per thread, grid-strided, 256
  * workgroups of 1024 threads (the best read-only shape measured on gfx950,
  * DESIGN.md §4) -- so that a benchmark can time the HBM read rate beside the

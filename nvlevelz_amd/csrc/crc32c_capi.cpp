@@ -1091,7 +1091,7 @@ int nvl_crc32c_fill_splitmix(void* dst, uint64_t nblocks, uint64_t block_bytes, 
 
 int nvl_crc32c_read_probe(const void* src, uint64_t bytes, uint32_t* sink, void* stream) {
   if (bytes == 0) return NVL_CRC32C_OK;
-  if (!src || !sink || (bytes % 16) != 0) return NVL_CRC32C_EINVAL;
+  if (!src || !sink || (bytes % 16) != 0 || (reinterpret_cast<uintptr_t>(src) % 16) != 0) return NVL_CRC32C_EINVAL;
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return NVL_CRC32C_ENODEV;
   return hip_rc(launch_read_probe(src, bytes, sink, static_cast<hipStream_t>(stream)));

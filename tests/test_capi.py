@@ -101,6 +101,12 @@ def test_argument_errors(L):
     assert L.lib.nvl_crc32c_fixed_dev(None, 0, 0, 0, None, 0, None, 0, None, 0, None) in (0, L.ENODEV)
     assert L.lib.nvl_crc32c_fill_splitmix(None, 1, 8, 0, 1, 0, None) == L.EINVAL
     assert L.lib.nvl_crc32c_fill_splitmix(ctypes.c_void_p(16), 1, 7, 0, 1, 0, None) == L.EINVAL
+    # the read probe (bench.py's ceiling): whole 16-byte granules from a 16-byte-aligned source, a sink
+    assert L.lib.nvl_crc32c_read_probe(None, 0, None, None) == 0
+    assert L.lib.nvl_crc32c_read_probe(ctypes.c_void_p(16), 24, ctypes.c_void_p(16), None) == L.EINVAL
+    assert L.lib.nvl_crc32c_read_probe(ctypes.c_void_p(24), 32, ctypes.c_void_p(16), None) == L.EINVAL
+    assert L.lib.nvl_crc32c_read_probe(ctypes.c_void_p(16), 32, None, None) == L.EINVAL
+    assert L.lib.nvl_crc32c_read_probe(ctypes.c_void_p(16), 32, ctypes.c_void_p(16), None) in (L.ENODEV, L.EHIP)
 
 
 def test_product_does_not_import_oracle():

@@ -5,6 +5,7 @@
 // (HIP events), in us and TB/s.  Build: hipcc -O3 --offload-arch=gfx950
 // tools/diag/hbm_ceiling.hip -o tools/diag/hbm_ceiling
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -110,6 +111,23 @@ __global__ void blocks_rows_adj_k(const uint8_t* __restrict__ p, uint64_t nblock
   if (x == 0x12345678u) out[0] = x;
 }
 
+// blocks_k with a dynamic LDS allocation that caps workgroups per CU
+// (occupancy sweep: waves per CU at 1 or 2 workgroups per CU)
+__global__ void blocks_dyn_k(const uint8_t* __restrict__ p, uint64_t nblocks, uint32_t* out) {
+  extern __shared__ uint32_t dyn[];
+  uint32_t x = 0;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (uint64_t b = (uint64_t)blockIdx.x * nw + wv; b < nblocks; b += (uint64_t)gridDim.x * nw) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(p + b * 4096u);
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = __builtin_nontemporal_load(q + 64 * j + lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+  }
+  if (x == 0x12345678u) { dyn[threadIdx.x] = x; out[0] = dyn[(threadIdx.x + 1) % blockDim.x]; }
+}
+
 template <class F>
 static float period(F launch, int R = 200) {
   hipEvent_t a, b;
@@ -138,6 +156,25 @@ int main() {
            (unsigned long long)bytes, us, bytes / (us * 1e-6) / 1e12, bytes / (us * 1e-6) / 8e12);
   };
   const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  if (getenv("OCC_SWEEP")) {
+    (void)hipFuncSetAttribute((const void*)blocks_dyn_k, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    char what[128];
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int T : {1024, 768}) {  // one workgroup per CU (100 KiB LDS)
+        snprintf(what, sizeof what, "4 KiB blocks per wave, 256 x %d, 1 WG/CU (%d waves/CU)", T, T / 64);
+        rep(what, period([&] { hipLaunchKernelGGL(blocks_dyn_k, dim3(256), dim3(T), 100 * 1024, 0, p, nblk, out); }));
+      }
+      for (int T : {512, 640, 768, 896, 1024}) {  // two per CU (72 KiB LDS)
+        snprintf(what, sizeof what, "4 KiB blocks per wave, 512 x %d, 2 WG/CU (%d waves/CU)", T, 2 * T / 64);
+        rep(what, period([&] { hipLaunchKernelGGL(blocks_dyn_k, dim3(512), dim3(T), 72 * 1024, 0, p, nblk, out); }));
+      }
+      for (int T : {256, 320, 384}) {  // four per CU (36 KiB LDS)
+        snprintf(what, sizeof what, "4 KiB blocks per wave, 1024 x %d, 4 WG/CU (%d waves/CU)", T, 4 * T / 64);
+        rep(what, period([&] { hipLaunchKernelGGL(blocks_dyn_k, dim3(1024), dim3(T), 36 * 1024, 0, p, nblk, out); }));
+      }
+    }
+    return 0;
+  }
   for (int pass = 0; pass < 2; ++pass) {
     rep("grid-stride 256 x 1024, 1 x 16 B nt", period([&] { hipLaunchKernelGGL((stream_k<1, true>), dim3(256), dim3(1024), 0, 0, q, n16, out); }));
     rep("grid-stride 256 x 1024, 4 x 16 B nt", period([&] { hipLaunchKernelGGL((stream_k<4, true>), dim3(256), dim3(1024), 0, 0, q, n16, out); }));

@@ -211,8 +211,9 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   //    index block's offset (between the meta blocks and the first piece, so
   //    the slots stay in file order); a meta slot that is not read gets length
   //    0 at the previous slot's end for the same reason.  (A table whose
-  //    blocks are out of file order still verifies: the region path then
-  //    checksums the batch serially, correct and slow.)
+  //    blocks are out of file order still verifies: nvl_crc32c_region_dev's
+  //    plan finds the batch not region-shaped and runs it on the batch
+  //    kernels)
   const uint64_t nf = nm_max;
   uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
   uint8_t* mv = pin + p_slots + nf * 16;

@@ -2247,6 +2247,7 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_head_kernel(G g, KArgs ka)
 constexpr int kFastU = 2;  // buffers per unit in scheduler A (tools/ab_bench.py: 2 > 1 > 4)
 
 constexpr int kGenWaves = 16;  // waves per workgroup of the kGeneral kernels
+constexpr int kGenPairU = 2;   // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 91.7 through run_units)
 template <int M>
 constexpr int waves_of() { return M == kGeneral ? kGenWaves : kWavesPerWG; }
 
@@ -2259,7 +2260,6 @@ __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(
       return;
     }
   }
-constexpr int kGenPairU = 2;  // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 91.7 through run_units)
   if constexpr (M == kGeneral) {
     // one whole chunk per buffer (len == 4096, any alignment): scheduler A,
     // one buffer per unit, no records

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 export PMC_SET=quick NVL_CRC32C_SELFTEST_REPORT_ONLY=1
 for v in base noquad; do
-  bash tools/pmc.sh q_$v --lib build/libnvl_crc32c_$v.so --config rand --region --shaped --launches 10 \
+  bash tools/pmc.sh q_$v --lib $R/build/libnvl_crc32c_$v.so --config rand --region --shaped --launches 10 \
     > gpurun_out/pmc_q_$v.log 2>&1 || { echo "pmc $v failed"; tail -5 gpurun_out/pmc_q_$v.log; exit 1; }
   echo "pmc $v ok"
 done

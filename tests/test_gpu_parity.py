@@ -525,3 +525,32 @@ def test_fixed_masked_pairs_overlapping(dev, C, port, length, stride, n):
                               base_offset=base_off))
     want = port.fixed(host[base_off:], stride, length, n, inits)
     assert np.array_equal(got, want)
+
+
+def test_read_probe_reads_every_granule(dev):
+    """nvl_crc32c_read_probe (bench.py's measured read ceiling) XORs every
+    16-byte granule a thread reads (granules t, t + S, t + 2S, ..., S = 256 x
+    1024 threads) and writes its sink only when that XOR is 0x12345678.  The
+    pattern split over two granules S apart -- the last one and the one a
+    stride before it -- reaches the sink only if that thread read both, in
+    the four-load main loop, the tail loop, or across them."""
+    from nvlevelz_amd import _lib
+    lib = _lib.lib
+    st = torch.cuda.current_stream().cuda_stream
+    S = 256 * 1024
+    for n16 in (1, 4 * S + 5, 8 * S, 9 * S - 1):
+        buf = torch.zeros(n16 * 4, dtype=torch.int32, device=dev)
+        if n16 == 1:
+            buf[0] = 0x12345678
+        else:
+            buf[4 * (n16 - 1)] = 0x12340000
+            buf[4 * (n16 - 1 - S) + 3] = 0x5678
+        sink = torch.zeros(1, dtype=torch.int32, device=dev)
+        assert lib.nvl_crc32c_read_probe(buf.data_ptr(), n16 * 16, sink.data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        assert int(sink.item()) == 0x12345678, n16
+        buf[4 * (n16 - 1) + 1] = 1  # now no thread's XOR is the pattern
+        sink.zero_()
+        assert lib.nvl_crc32c_read_probe(buf.data_ptr(), n16 * 16, sink.data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        assert int(sink.item()) == 0, n16

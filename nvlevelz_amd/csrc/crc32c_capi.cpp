@@ -615,9 +615,6 @@ bool thread_table_aux(int device, hipStream_t* side, hipEvent_t* ev_a, hipEvent_
   return *side && e[0] && e[1];
 }
 
-namespace {
-
-}  // namespace
 }  // namespace nvl
 
 using namespace nvl;

@@ -156,7 +156,10 @@ NVL_API size_t nvl_crc32c_fixed_workspace_bytes(uint64_t stride, uint64_t len, u
  * buffers' own pages are read: buffers from different allocations are safe),
  * gaps between buffers at most 1/8 of the buffer bytes + 64 KiB, a span of
  * at most 64 GiB -- is checksummed over its own span by the region path (see
- * nvl_crc32c_region_dev), any other by the batch kernels. */
+ * nvl_crc32c_region_dev); any other batch whose buffers are all exactly 4096
+ * bytes (shuffled blocks, pages far apart or overlapping) by the page path
+ * (one 4 KiB pass per buffer at the fixed-stride path's rate); the rest by
+ * the batch kernels. */
 NVL_API int nvl_crc32c_batch_dev(const void* base, const uint64_t* offsets, const uint64_t* lengths,
                          const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* workspace, size_t workspace_bytes,
@@ -176,7 +179,8 @@ NVL_API size_t nvl_crc32c_batch_workspace_bytes(uint64_t n);
  * their bytes (the whole region is read).  The layout is checked on the
  * device first: a batch that is not region-shaped (unsorted, overlapping, a
  * buffer outside the region or longer than NVL_CRC32C_REGION_MAX_LEN) runs
- * the batch kernels of nvl_crc32c_batch_dev.  NVL_CRC32C_FLAG_REGION_SHAPED
+ * as nvl_crc32c_batch_dev runs it (the page path or the batch kernels).
+ * NVL_CRC32C_FLAG_REGION_SHAPED
  * skips the check (one launch instead of three). */
 NVL_API int nvl_crc32c_region_dev(const void* region, uint64_t region_len, const uint64_t* offsets,
                                   const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,

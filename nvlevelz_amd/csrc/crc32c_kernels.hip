@@ -294,14 +294,21 @@ __device__ __forceinline__ T ldc(const T* p, uint64_t i) {
 // Route plan of a batch over device metadata (nvl_crc32c_batch_dev,
 // nvl_crc32c_region_dev): crc32c_route_plan checks the offsets and lengths
 // in slices and writes one partial per slice; every later launch of the
-// call reduces the same partials (route_region: one wave-wide load, a ballot
+// call reduces the same partials (route_region: one wave-wide load, ballots
 // and a sum) and takes the same decision -- the region path for a
 // region-shaped batch, the head + body kernels otherwise.  No atomics, no
 // reset: the partials are plain stores of the plan launch.
 struct RoutePart {
   uint64_t sum;  // sum of the slice's lengths, each capped at kRegionMaxLen + 1 (< 2^43 for n < 2^31)
-  uint64_t bad;  // 1: a pair out of order / overlapping, a buffer outside the region or longer than kRegionMaxLen
+  uint64_t bad;  // kRpBad | kRpNot4k | kRpUnaligned, OR over the slice
 };
+constexpr uint64_t kRpBad = 1;        // a pair out of order / overlapping, a buffer outside the region or too long
+constexpr uint64_t kRpNot4k = 2;      // a buffer whose length is not 4096
+constexpr uint64_t kRpUnaligned = 4;  // a buffer not 16-byte aligned
+// The launches after the plan: the region path, the page path (every buffer
+// exactly one 4 KiB chunk: scheduler A over the batch's own list, aligned or
+// realigned), or the head + body kernels.
+enum RouteKind : int { kRouteHeads = 0, kRouteRegion = 1, kRoutePages = 2, kRoutePagesAligned = 3 };
 constexpr uint32_t kRoutePlanMax = 128;  // plan workgroups (a wave reduces their partials, two per lane)
 struct Route {
   const RoutePart* parts = nullptr;  // nullptr: no route (the launch is what it is)
@@ -368,9 +375,12 @@ __device__ __forceinline__ uint64_t wave_total_u64(uint64_t v) {
 
 
 // The verdict, as every launch after the plan takes it: the partials (lane
-// k < np loads slice k's), a ballot of their bad flags and a sum of their
+// k < np loads slice k's), ballots of their flags and a sum of their
 // lengths; a sorted batch's span is [offsets[0], offsets[n-1] + lengths[n-1]).
-// lo / hi: the span (dyn).
+// lo / hi: the span (dyn).  Region-shaped: the region path.  Otherwise, when
+// every buffer is exactly 4096 bytes (pages of a block cache, a shuffled
+// batch of 4 KiB blocks, blocks far apart), the page path; else the head +
+// body kernels.
 __device__ __forceinline__ bool route_region(const Route& r, uint64_t& lo, uint64_t& hi) {
   const int lane = (int)(threadIdx.x & 63u);
   // lane k takes partials k, k + 64, ... (np <= kRoutePlanMax; the loads together, clamped)
@@ -385,7 +395,7 @@ __device__ __forceinline__ bool route_region(const Route& r, uint64_t& lo, uint6
 #pragma unroll
   for (uint32_t m = 0; m < kRoutePlanMax / 64u; ++m) {
     const bool mine = 64u * m + (uint32_t)lane < r.np;
-    bad |= mine && q[m].bad != 0u;
+    bad |= mine && (q[m].bad & kRpBad) != 0u;
     some |= mine && q[m].sum != 0u;
     lsum += mine ? q[m].sum : 0u;
   }
@@ -397,6 +407,17 @@ __device__ __forceinline__ bool route_region(const Route& r, uint64_t& lo, uint6
   if (hi - lo - sum > sum / 8u + 65536u) return false;
   const uintptr_t O = ((uintptr_t)r.base + lo) & ~(uintptr_t)(kChunk - 1u);
   return ((uintptr_t)r.base + hi - O + kChunk - 1u) / kChunk <= r.cap_chunks;
+}
+// Not region-shaped: the page path (kRoutePages / kRoutePagesAligned) or the
+// head + body kernels (kRouteHeads), from the partials' flags.
+__device__ __forceinline__ int route_other(const Route& r) {
+  const int lane = (int)(threadIdx.x & 63u);
+  uint64_t fl = 0;
+#pragma unroll
+  for (uint32_t m = 0; m < kRoutePlanMax / 64u; ++m)
+    if (m == 0u || 64u * m < r.np) fl |= 64u * m + (uint32_t)lane < r.np ? r.parts[min(64u * m + (uint32_t)lane, r.np - 1u)].bad : 0u;
+  if (__ballot((fl & kRpNot4k) != 0u)) return kRouteHeads;
+  return __ballot((fl & kRpUnaligned) != 0u) ? kRoutePages : kRoutePagesAligned;
 }
 
 
@@ -2814,6 +2835,16 @@ __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(
   if (ka.route.parts) {
     uint64_t lo, hi;
     if (route_region(ka.route, lo, hi)) return;  // the region path ran
+    const int rv = route_other(ka.route);
+    if (rv == kRoutePagesAligned) {  // every buffer one aligned 4 KiB chunk: config 2's loop over the list
+      run_pairs<kFastU, kGenWaves, kAligned, VarGeom>(gv, ka, lds);  // (the kLdsBytes image: the region one
+                                                                     // and this kernel's own LDS exceed 160 KiB)
+      return;
+    }
+    if (rv == kRoutePages) {  // every buffer 4096 bytes, some misaligned
+      run_pairs<kGenPairU, kGenWaves, kGeneral, VarGeom>(gv, ka, lds);
+      return;
+    }
   }
   const uint32_t ub0 = blockIdx.x * kUnitsPerWG;
   uint64_t C0, C1, B0, B1;
@@ -3701,7 +3732,7 @@ __global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __re
   const uint64_t P = gridDim.x, k = blockIdx.x;
   const uint64_t i0 = n * k / P, i1 = n * (k + 1) / P;
   uint64_t sum = 0;  // (lengths capped at kRegionMaxLen + 1: a longer one makes the slice bad anyway)
-  bool bad = false;
+  bool bad = false, not4k = false, unal = false;
   for (uint64_t b = i0 + (uint64_t)threadIdx.x * kPlanPer; b < i1; b += (uint64_t)kPlanT * kPlanPer) {
     uint64_t o[kPlanPer + 1], L[kPlanPer + 1];
 #pragma unroll
@@ -3723,15 +3754,18 @@ __global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __re
         }
       }
       if (pages && b + q == 0u) bad |= L[q] == 0u;
+      not4k |= L[q] != (uint64_t)kChunk;
+      unal |= ((base + o[q]) & 15u) != 0u;
       sum += min<uint64_t>(L[q], kRegionMaxLen + 1u);
     }
   }
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t tot = wave_total_u64(sum);
-  const bool wb = __ballot(bad) != 0u;
+  const uint32_t wb = (__ballot(bad) ? (uint32_t)kRpBad : 0u) | (__ballot(not4k) ? (uint32_t)kRpNot4k : 0u) |
+                      (__ballot(unal) ? (uint32_t)kRpUnaligned : 0u);
   if (lane == 0u) {
     wsum[w] = tot;
-    wbad[w] = wb ? 1u : 0u;
+    wbad[w] = wb;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3766,10 +3800,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg
     const uint32_t G = (uint32_t)max<uint64_t>(1u, min<uint64_t>(gridDim.x, gw));
     if (blockIdx.x >= G) return;
     run_region<kFastU>(rg, ka, lds, G);
-  } else {
+  } else if (route_other(ka.route) == kRouteHeads) {
     if (blockIdx.x >= ka.tile_G) return;
     run_heads(vg, ka, lds);
-  }
+  }  // (the page path runs in crc32c_var_fused_kernel: here its registers would spill the region path's SGPRs)
 }
 
 // The read ceiling probe (nvl_crc32c_read_probe): grid-strided, four
@@ -4128,7 +4162,7 @@ static uint32_t next_generation() {
 size_t route_parts_bytes() { return (dev::kRoutePlanMax * sizeof(dev::RoutePart) + 255u) / 256u * 256u; }
 // Region chunks a region-shaped batch_dev batch can span: sorted, each buffer
 // <= kRegionMaxLen (32 chunks), gaps <= 1/8 of the bytes + 64 KiB -> at most
-// 36 chunks per buffer + 18 + 2 (route_verdict checks it).
+// 36 chunks per buffer + 18 + 2 (route_region checks it).
 // Capped at 2^24 chunks (64 MiB of raws, a 64 GiB span): a larger batch
 // takes the batch path rather than a workspace of 4 bytes per 4 KiB of the
 // worst case (10^7 buffers would have reserved 1.4 GB).

@@ -703,6 +703,18 @@ def route_region_ok(offs, lens, lim: int, base: int, dyn: bool, cap_chunks: int)
     return (base + hi - O + 4095) // 4096 <= cap_chunks
 
 
+def route_verdict(offs, lens, lim: int, base: int, dyn: bool, cap_chunks: int) -> str:
+    """route_verdict: the region path for a region-shaped batch; else the
+    page path when every buffer is exactly 4096 bytes ("pages_aligned" when
+    every one is 16-byte aligned at A(x) = base + x); else the head + body
+    kernels."""
+    if route_region_ok(offs, lens, lim, base, dyn, cap_chunks):
+        return "region"
+    if all(int(x) == 4096 for x in lens):
+        return "pages_aligned" if all((base + int(o)) % 16 == 0 for o in offs) else "pages"
+    return "heads"
+
+
 def span_pages_touched(offs, lens, base: int) -> bool:
     """Every 4 KiB page of the span [A(offsets[0]), A(end of the last)) holds
     a byte of some non-empty buffer (brute force)."""

@@ -327,3 +327,29 @@ def test_million_small_buffers(dev, C, port):
     offs2[[j, j + 1]] = offs2[[j + 1, j]]
     lens2[[j, j + 1]] = lens2[[j + 1, j]]
     _both(C, dev, port, host, buf, offs2, lens2, 4)
+
+
+@pytest.mark.parametrize("case", ["shuffled", "shuffled_odd", "strided", "overlapping", "small", "large_shuffled",
+                                  "one_not_4096"])
+def test_page_route(dev, C, port, case):
+    """Batches of exactly-4096-byte buffers that are not region-shaped take
+    the page path (scheduler A over the batch's own list, in the body
+    kernel): shuffled, from an odd base (realigned passes),
+    sorted but far apart (the gap rule fails), overlapping, a handful, 10^5
+    shuffled; and with one 4095-byte buffer among them, the head + body
+    kernels.  Every CRC against the oracle, with per-buffer init and the mask."""
+    rng = np.random.default_rng(abs(hash(case)) & 0xFFFF)
+    n = {"small": 5, "large_shuffled": 100_000}.get(case, 3000)
+    lead = 3 if case == "shuffled_odd" else 0
+    step = {"strided": 12288, "overlapping": 2048}.get(case, 4096)
+    offs = lead + step * np.arange(n, dtype=np.int64)
+    lens = np.full(n, 4096, dtype=np.int64)
+    if case not in ("strided", "overlapping"):
+        p = rng.permutation(n)
+        offs = offs[p]
+    if case == "one_not_4096":
+        lens[n // 2] = 4095
+    total = int(offs.max() + 4096 + 64)
+    host = rng.integers(0, 256, size=total, dtype=np.uint8)
+    buf = torch.from_numpy(host).to(dev)
+    _both(C, dev, port, host, buf, offs, lens, seed=n + step, mask=(case == "shuffled"))

@@ -85,3 +85,25 @@ def test_call_site_shapes_accepted():
     offs = _packed(lens, 1 << 20)
     assert km.route_plan_bad(offs, lens, NOLIM, 0, True)
     assert not km.route_plan_bad(offs, lens, NOLIM, 0, False)
+
+
+def test_page_route_verdicts():
+    """The page path takes what the region path does not, when every buffer
+    is exactly 4096 bytes; a region-shaped batch of pages stays on the
+    region path (it reads the same bytes, from one span)."""
+    base = 1 << 30
+    cap = lambda n: 36 * n + 20
+    packed = 4096 * np.arange(64)
+    assert km.route_verdict(packed, [4096] * 64, NOLIM, base, True, cap(64)) == "region"
+    shuffled = packed[::-1]
+    assert km.route_verdict(shuffled, [4096] * 64, NOLIM, base, True, cap(64)) == "pages_aligned"
+    assert km.route_verdict(shuffled + 3, [4096] * 64, NOLIM, base, True, cap(64)) == "pages"
+    far = 3 * packed  # sorted, gaps twice the bytes: the gap rule fails
+    assert km.route_verdict(far, [4096] * 64, NOLIM, base, True, cap(64)) == "pages_aligned"
+    over = 2048 * np.arange(64)  # overlapping
+    assert km.route_verdict(over, [4096] * 64, NOLIM, base, True, cap(64)) == "pages_aligned"
+    lens = [4096] * 64
+    lens[7] = 4095
+    assert km.route_verdict(shuffled, lens, NOLIM, base, True, cap(64)) == "heads"
+    # region_dev (the caller's region): out of the region is not region-shaped
+    assert km.route_verdict(packed, [4096] * 64, 4096 * 63, base, False, 0) == "pages_aligned"

@@ -6,7 +6,8 @@ around each call, median of R reps), every result checked.
            region path, the body kernel's early exit)
   3S, vS, rS  the same with NVL_CRC32C_FLAG_REGION_SHAPED (the region kernel alone, one launch)
   u, uR    10^5 x 4 KiB at 4 KiB-aligned offsets in a random order (not region-shaped) through
-           nvl_crc32c_batch_dev / nvl_crc32c_region_dev (both: plan, then the batch kernels)
+           nvl_crc32c_batch_dev / nvl_crc32c_region_dev (both: plan, then the page path)
+  uo       u from an odd base (the page path's realigned passes), nvl_crc32c_batch_dev
   big1     one aligned 1 GiB buffer (fixed path, n = 1)
   v        10^5 x 4097 B at stride 4101: block | type of 4096-byte SSTable blocks with their
            4-byte stored CRC between them (whole-table verify shape), nvl_crc32c_batch_dev
@@ -119,7 +120,7 @@ for c in a.configs.split(","):
         buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"], region=c != "3", shaped=c == "3S")
         alg = total + 12 * n
         check = lambda res: p.digest(res) == cfg["digest"]
-    elif c in ("v", "r", "vR", "rR", "vS", "rS", "u", "uR"):
+    elif c in ("v", "r", "vR", "rR", "vS", "rS", "u", "uR", "uo"):
         n = 100_000
         if c[0] == "v":
             lens = np.full(n, 4097, dtype=np.int64)
@@ -128,8 +129,8 @@ for c in a.configs.split(","):
         else:
             lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
         if c[0] == "u":
-            offs = np.random.default_rng(8).permutation(n).astype(np.int64) * 4096
-            total = n * 4096
+            offs = np.random.default_rng(8).permutation(n).astype(np.int64) * 4096 + (3 if c == "uo" else 0)
+            total = n * 4096 + (3 if c == "uo" else 0)
         else:
             offs = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
             total = int(offs[-1] + lens[-1]) + 4

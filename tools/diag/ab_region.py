@@ -1,5 +1,5 @@
 """Interleaved timing of library variants on the region path (one process):
-    python tools/diag/ab_region.py CONFIG lib_A.so lib_B.so ...   (CONFIG: vR, rR, 3R)
+    python tools/diag/ab_region.py CONFIG lib_A.so lib_B.so ...   (CONFIG: vR, rR, 3R, uR, uoR)
 M rounds x R back-to-back calls per variant, HIP events around each round
 (mean per call = the sustained period) and around single calls (median)."""
 import ctypes, json, os, sys
@@ -30,6 +30,10 @@ else:
             ).astype(np.int64); gap = 4
     total = int((lens + gap).sum()); alg = int(lens.sum()) + 20 * lens.size
 offs = np.concatenate([[0], np.cumsum(lens + gap)[:-1]]).astype(np.int64)
+if cfg in ("uR", "uoR"):  # 10^5 x 4096 B shuffled (not region-shaped: the page path), uoR from an odd base
+    lens = np.full(100_000, 4096, dtype=np.int64)
+    offs = (4096 * np.random.default_rng(1).permutation(lens.size) + (3 if cfg == "uoR" else 0)).astype(np.int64)
+    total = int(offs.max()) + 4096; alg = int(lens.sum()) + 20 * lens.size
 n = lens.size
 buf = torch.empty(total + 64, dtype=torch.uint8, device=dev)
 libs[0].nvl_crc32c_fill_splitmix(buf.data_ptr(), (total + 64) // 8, 8, 0, 1, 0x5EED00B1, None)

@@ -8,7 +8,7 @@
 #   prof    rocprofv3 --kernel-trace --stats of that same command (summary split by phase)
 #   spawn   self-spawned 2-rank rehearsals without torchrun (gloo, ranks sharing one GPU):
 #           cfg5 (full 10^7-block digest through shard.gather_crcs) and cfg2
-#   configs tools/bench_configs.py over 2,3,3R,3S,4,v,vR,vS,r,rR,rS,g,u,uR,big1
+#   configs tools/bench_configs.py over 2,3,3R,3S,4,v,vR,vS,r,rR,rS,g,u,uR,uo,big1
 #   shims   rocprofv3 kernel trace of the whole-table verify shim bench
 #   smoke   __graft_entry__.smoke();  default  python3 bench.py with no flags (the driver's BENCH line)
 #   pmc     tools/pmc.sh (full counter set) on cfg2, rand (3364..4109 B), var4097, cfg3
@@ -47,7 +47,7 @@ for s in $STEPS; do
     spawn)
       NVL_BENCH_BACKEND=gloo run spawn_cfg5 400 python3 bench.py --gpus 2 --config cfg5 --steps 10 --warmup 2 --no-cpu --no-e2e
       NVL_BENCH_BACKEND=gloo run spawn_cfg2 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-e2e ;;
-    configs) run configs 600 python3 tools/bench_configs.py --configs 2,3,3R,3S,4,v,vR,vS,r,rR,rS,g,u,uR,big1 ;;
+    configs) run configs 600 python3 tools/bench_configs.py --configs 2,3,3R,3S,4,v,vR,vS,r,rR,rS,g,u,uR,uo,big1 ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     ceiling) run ceiling 120 ./tools/diag/hbm_ceiling ;;
     default) run bench_default 400 python3 bench.py ;;

@@ -1,6 +1,7 @@
 """Randomised routed calls: 400 batches of random shape --
 sorted and dense, sorted with gaps (some over a page), unsorted, overlapping,
-with empty buffers, long buffers over the 128 KiB limit, tiny and large n --
+with empty buffers, long buffers over the 128 KiB limit, tiny and large n,
+exactly-4096-byte buffers anywhere (the page path) --
 through nvl_crc32c_batch_dev and nvl_crc32c_region_dev on one stream and ONE
 reused workspace, every CRC against the oracle.  Back-to-back calls of
 different layouts share the workspace's plan partials and event records, so
@@ -29,8 +30,16 @@ def _t64(a, dev):
 
 
 def _batch(rng, image):
-    kind = rng.integers(0, 6)
+    kind = rng.integers(0, 7)
     n = int(rng.choice([1, 2, 7, 63, 64, 65, 500, 3000, 20_000, 70_000]))
+    if kind == 6:  # exactly-4096-byte buffers anywhere (the page path unless region-shaped): random
+        # positions on a 4 KiB, 16-byte or 1-byte grid -- in any order, overlapping -- or packed
+        g = int(rng.choice([4096, 16, 1]))
+        if rng.random() < 0.2:
+            offs = 4096 * np.arange(min(n, image // 4096 - 1)) + int(rng.integers(0, 64)) * g % 4096
+        else:
+            offs = rng.integers(0, (image - 4096) // g, n) * g
+        return offs.astype(np.int64), np.full(len(offs), 4096, dtype=np.int64)
     if kind == 4:  # long buffers, some over the region path's 128 KiB limit
         lens = rng.integers(1, 300_000, n)
     elif kind == 5:  # tiny

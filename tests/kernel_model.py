@@ -726,3 +726,63 @@ def span_pages_touched(offs, lens, base: int) -> bool:
         if L:
             touched.update(range((base + int(o)) >> 12, ((base + int(o) + int(L) - 1) >> 12) + 1))
     return all(p in touched for p in range(lo >> 12, ((hi - 1) >> 12) + 1))
+
+
+# ---- the compact LDS image (64 KiB; tools/diag/compact_steal.patch) ---------
+
+def perm(s0: int, s1: int, sel: int) -> int:
+    """v_perm_b32 for selector bytes 0..7 and 0x0C: bytes 0-3 of s1, 4-7 of
+    s0, 0x0C gives 0x00."""
+    src = s1.to_bytes(4, "little") + s0.to_bytes(4, "little")
+    out = 0
+    for i in range(4):
+        c = (sel >> (8 * i)) & 0xFF
+        out |= (src[c] if c < 8 else 0) << (8 * i)
+    return out
+
+
+def compact_image():
+    """Dword image of kCLdsBytes as fill_compact_load/store write it: row b
+    (256 B): slots j*8 + r = T[3 - j][b]; bytes 128.. of row 16n + v + 128h:
+    T[n][v][32h + c] at dword 32 + c (lane 63's column left as the counter)."""
+    img = [0] * 16384
+    for b in range(256):
+        for j in range(4):
+            for r in range(8):
+                img[b * 64 + j * 8 + r] = T[3 - j][b]
+    for h in range(2):
+        for n in range(8):
+            for v in range(16):
+                row = 16 * n + v + 128 * h
+                for c in range(32):
+                    img[row * 64 + 32 + c] = nibble_table(n, v, 32 * h + c)
+    return img
+
+
+def compact_lane_base(lane: int):
+    r = (lane >> 2) & 7
+    B = (r * 4) | ((8 + r) * 4) << 8 | ((16 + r) * 4) << 16 | ((24 + r) * 4) << 24
+    sels = []
+    for k in range(4):
+        j = (k + lane) & 3
+        sels.append(j | (4 + j) << 8 | 0x0C0C0000)
+    return B, sels
+
+
+def compact_slice4_addrs(x: int, lane: int):
+    """Byte addresses of the four lookups of slice4c_next (k = 0..3)."""
+    B, sels = compact_lane_base(lane)
+    return [perm(x, B, s) for s in sels]
+
+
+def compact_nibble_addrs(lr: int, lane: int):
+    """Byte addresses of to_chunk_end_c's eight lookups (image + 128 + n*4096)."""
+    jb = (lane & 31) << 2
+    hb = 0x80808080 if lane >= 32 else 0
+    lo = (lr & 0x0F0F0F0F) | hb
+    hi = ((lr >> 4) & 0x0F0F0F0F) | hb
+    out = []
+    for n in range(8):
+        src = lo if n % 2 == 0 else hi
+        out.append(128 + n * 4096 + perm(src, jb, 0x0C0C0400 | (n // 2) << 8))
+    return out

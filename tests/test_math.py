@@ -288,3 +288,39 @@ def test_region_stale_halo_origin_addresses_past_the_region():
             for f, c in [km.region_span_stale(u, B0, nfull, nunits, nhalo, hc)] for k in range(c)]
     assert max(addr) >= nc  # past the region: the illegal address
     km.region_schedule(starts, lens, rel0, lens[0] + starts[0], G)  # the shipped span_of stays inside
+
+
+def test_compact_image_lookups_and_banks():
+    """The 64 KiB image of tools/diag/compact_steal.patch (two workgroups per
+    CU; measured, not shipped -- DESIGN §8): each lane's four slice
+    lookups (bytes taken in the lane's rotated order) sum to slice4(x), its
+    eight nibble lookups to the lane's shift to the chunk end, and every
+    ds_read_b32 of a wave hits 32 distinct banks ((a/4) mod 32) in each
+    32-lane group, whatever the data."""
+    img = km.compact_image()
+    rng = random.Random(5)
+    for trial in range(40):
+        xs = [rng.getrandbits(32) for _ in range(64)]
+        addrs = [km.compact_slice4_addrs(xs[l], l) for l in range(64)]
+        for l in range(64):
+            a = addrs[l]
+            assert all(0 <= v < 65536 and v % 4 == 0 and (v & 255) < 128 for v in a)
+            got = 0
+            for v in a:
+                got ^= img[v // 4]
+            assert got == km.slice4(xs[l])
+        for k in range(4):
+            for g in (range(32), range(32, 64)):
+                assert len({(addrs[l][k] // 4) % 32 for l in g}) == 32
+        nad = [km.compact_nibble_addrs(xs[l], l) for l in range(64)]
+        for l in range(63):  # lane 63: identity, its column is the counter
+            got = 0
+            for v in nad[l]:
+                assert 0 <= v < 65536 and (v & 255) >= 128
+                got ^= img[v // 4]
+            assert got == km.shift(xs[l], 64 * (63 - l))
+        for n in range(8):
+            for g in (range(32), range(32, 64)):
+                assert len({(nad[l][n] // 4) % 32 for l in g}) == 32
+    ctr = (128 * 256 + 128 + 31 * 4) // 4  # kCCtrOff: lane 63's slot, row (n=0, v=0, h=1)
+    assert ctr == 128 * 64 + 32 + 31

@@ -27,7 +27,7 @@ def main():
     buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
     libs[0].nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, 0x5EED0001, None)
     outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
-    ws = torch.empty(max(1, libs[0].nvl_crc32c_fixed_workspace_bytes(L, L, n)), dtype=torch.uint8, device=dev)
+    ws = torch.empty(max([1] + [lib.nvl_crc32c_fixed_workspace_bytes(L, L, n) for lib in libs]), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     def run(k):
         rc = libs[k].nvl_crc32c_fixed_dev(buf.data_ptr(), L, L, n, None, 0, outs[k].data_ptr(), 0,

@@ -24,7 +24,8 @@ lib.nvl_crc32c_fill_splitmix(buf.data_ptr(), n, L, 0, 1, 0x5EED0001, None)
 out = torch.empty(n, dtype=torch.int32, device=dev)
 st = torch.cuda.current_stream().cuda_stream
 lib.nvl_diag_stamps.restype = ctypes.c_int
-h = np.zeros(4 * 4096, dtype=np.uint64)
+NWV = int(os.environ.get("NWAVES", "4096"))  # waves of the launch (compact kernel: 512 x 12 or 16)
+h = np.zeros(4 * NWV, dtype=np.uint64)
 rows = []
 for it in range(int(os.environ.get("ITERS", "30"))):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -35,7 +36,7 @@ for it in range(int(os.environ.get("ITERS", "30"))):
     torch.cuda.synchronize()
     ev = e0.elapsed_time(e1) * 1e3
     lib.nvl_diag_stamps(h.ctypes.data_as(ctypes.c_void_p), h.size)
-    s = h.reshape(-1, 4).astype(np.int64)[:16 * 256]
+    s = h.reshape(-1, 4).astype(np.int64)[:NWV]
     t0 = s[:, 0].min()
     start = (s[:, 0] - t0) / 100.0
     fill = (s[:, 1] - s[:, 0]) / 100.0
@@ -47,6 +48,11 @@ for it in range(int(os.environ.get("ITERS", "30"))):
          "fill_us_p50": round(float(np.median(fill)), 2), "fill_us_max": round(float(fill.max()), 2),
          "end_p50_us": round(float(np.median(end)), 2), "end_max_us": round(float(end.max()), 2),
          "xcd_end_us": [round(x, 2) for x in xend]}
+    cnt = (s[:, 3] & 0xFFFFFFFF).astype(np.float64)
+    busy = (s[:, 2] - s[:, 1]) / 100.0
+    r["units_p10_p50_p90"] = [float(np.percentile(cnt, q)) for q in (10, 50, 90)]
+    r["units_total"] = int(cnt.sum())
+    r["us_per_unit_p50"] = round(float(np.median(busy / np.maximum(cnt, 1))), 3)
     rows.append(r)
     print(json.dumps(r), flush=True)
 keys = ["event_us", "span_us", "outside_us", "start_spread_us", "fill_us_p50", "end_p50_us", "end_max_us"]

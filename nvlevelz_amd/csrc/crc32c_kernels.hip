@@ -244,6 +244,48 @@ __device__ __forceinline__ uint32_t shift4096(const uint8_t* lds, uint32_t acc, 
   return s;
 }
 
+// The same fill in two halves (loads, then stores), for a caller that issues
+// the blob's loads ahead of its first chunk loads (run_pairs).
+template <int NW>
+struct LdsFill {
+  uint32_t rep[(8192 + kWave * NW - 1) / (kWave * NW)];
+  uint4 op[(1792 + kWave * NW - 1) / (kWave * NW)];
+};
+template <int NW>
+__device__ __forceinline__ LdsFill<NW> fill_lds_load(const uint32_t* __restrict__ g) {
+  constexpr int kT = kWave * NW;
+  LdsFill<NW> f;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < (8192 + kT - 1) / kT; ++q) {
+    const uint32_t s = (uint32_t)(t + q * kT);
+    if ((8192 % kT) != 0 && s >= 8192u) break;
+    const uint32_t off = s << 4;
+    f.rep[q] = g[kGSlice + (((off >> 16) << 1) | ((off >> 7) & 1u)) * 256u + ((off >> 8) & 0xFFu)];
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
+#pragma unroll
+  for (int q = 0; q < (1792 + kT - 1) / kT; ++q)
+    if (t + q * kT < 1792) f.op[q] = src[t + q * kT];
+  return f;
+}
+template <int NW>
+__device__ __forceinline__ void fill_lds_store(uint8_t* lds, const LdsFill<NW>& f, uint32_t ctr0 = NW) {
+  constexpr int kT = kWave * NW;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < (8192 + kT - 1) / kT; ++q) {
+    const uint32_t s = (uint32_t)(t + q * kT);
+    if ((8192 % kT) != 0 && s >= 8192u) break;
+    *reinterpret_cast<uint4*>(lds + kSliceOff + (s << 4)) = make_uint4(f.rep[q], f.rep[q], f.rep[q], f.rep[q]);
+  }
+  uint4* dst = reinterpret_cast<uint4*>(lds + kCombOff);
+#pragma unroll
+  for (int q = 0; q < (1792 + kT - 1) / kT; ++q)
+    if (t + q * kT < 1792) dst[t + q * kT] = f.op[q];
+  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = ctr0;
+}
+
 // Fill the LDS image from the device table blob.
 template <int NW>
 __device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restrict__ g, uint32_t ctr0 = NW) {
@@ -1131,13 +1173,21 @@ __device__ __forceinline__ void run_pairs(const G& g, const KArgs& ka, uint8_t* 
   Pos gp[U];
   bool ok[U];
   Chunk cur[U];
+  // The table blob's loads go out ahead of the first unit's chunk loads, so
+  // the fill waits for them alone, not for the chunk burst queued in front
+  // (config 2 interleaved A/B: 63.6-63.7 vs 64.0 us back to back,
+  // profiles/r05b/ab_blobfirst.jsonl).
+  RegionFill rf;
+  LdsFill<NW> lf;
+  if constexpr (NIB) rf = fill_region_load(ka.tables);
+  else lf = fill_lds_load<NW>(ka.tables);
 #pragma unroll
   for (int k = 0; k < U; ++k) {
     ok[k] = unit_pos(u, k, gp[k]);
     if (ok[k]) load_chunk<M>(gp[k].bi, 0, lane, cur[k]);
   }
-  if constexpr (NIB) fill_region_store(lds, fill_region_load(ka.tables), NW);
-  else fill_lds<NW>(lds, ka.tables);
+  if constexpr (NIB) fill_region_store(lds, rf, NW);
+  else fill_lds_store<NW>(lds, lf, NW);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();

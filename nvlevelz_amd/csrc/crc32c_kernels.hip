@@ -1284,6 +1284,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
   // ends a unit prefetches the next unit's first step.  Every chunk load of the
   // loop is issued from one place, so the loaded registers carry straight into
   // the next iteration (no copies that would wait on the loads).
+  const LdsFill<NW> lf = fill_lds_load<NW>(ka.tables);  // ahead of the first chunk loads (run_pairs)
   uint32_t u = ub0 + wv;
   uint64_t t = lo_of(u), t1 = lo_of(u + 1);
   Pos p0{}, p1{};
@@ -1298,7 +1299,7 @@ __device__ __forceinline__ void run_units(const G& g, const KArgs& ka, uint8_t* 
       load_chunk<M>(p1.bi, p1.c, lane, c1);
     }
   }
-  fill_lds<NW>(lds, ka.tables);
+  fill_lds_store<NW>(lds, lf);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();
@@ -1569,9 +1570,10 @@ constexpr int kBufsTail = 0;  // single-buffer groups for the range's last buffe
   next_pos(p1);
   Chunk c0, c1;
   uint32_t hv0, hv1;
+  const LdsFill<NW> lf = fill_lds_load<NW>(ka.tables);  // ahead of the first chunk loads (run_pairs)
   load_pos(p0, lane, safe, ka.hc, c0, hv0);  // overlaps the LDS fill
   load_pos(p1, lane, safe, ka.hc, c1, hv1);
-  fill_lds<NW>(lds, ka.tables, 2u * NW);
+  fill_lds_store<NW>(lds, lf, 2u * NW);
   __syncthreads();
   const LaneBase lb = make_lane_base(lane);
   NVL_STAMP1();
@@ -2084,13 +2086,14 @@ __device__ __forceinline__ void run_heads(const G& g, const KArgs& ka, uint8_t* 
     a = s0 + (s1 - s0) * wv / kWavesPerWG;
     b = s0 + (s1 - s0) * (wv + 1) / kWavesPerWG;
   };
+  const LdsFill<kWavesPerWG> lf = fill_lds_load<kWavesPerWG>(ka.tables);  // ahead of the metadata loads
   {
     uint64_t a, b;
     slice(w0, min(w1, w0 + kHeadSub), a, b);
     if (a + (uint64_t)lane < b) g.lane_meta(a + (uint64_t)lane, lp, lL, ls);  // in flight during the fill
   }
   if (threadIdx.x < 4) ctl[threadIdx.x] = 0u;
-  fill_lds<kWavesPerWG>(lds, ka.tables);
+  fill_lds_store<kWavesPerWG>(lds, lf);
   // Every path passes this barrier before its first table lookup and its
   // first list append: it orders the LDS fill AND wave 0's zeroing of the
   // list counters ctl before them (round 3 faulted a parity test,

@@ -120,6 +120,18 @@ for c in a.configs.split(","):
         buf, out, fn, keep = varlen(offs, lens, total, cfg["seed"], region=c != "3", shaped=c == "3S")
         alg = total + 12 * n
         check = lambda res: p.digest(res) == cfg["digest"]
+    elif c == "rs":  # r's lengths packed in a shuffled order: not sorted, so batch_dev runs the batch kernels
+        n = 100_000
+        lens = np.random.default_rng(7).integers(3364, 4110, n).astype(np.int64)
+        perm = np.random.default_rng(9).permutation(n)
+        slot = np.concatenate([[0], np.cumsum(lens[perm] + 4)[:-1]])
+        offs = np.empty(n, dtype=np.int64)
+        offs[perm] = slot
+        total = int(slot[-1] + lens[perm[-1]]) + 4
+        buf, out, fn, keep = varlen(offs, lens, total, 0x5EED00B1)
+        alg = int(lens.sum()) + 20 * n
+        host = buf.cpu().numpy()
+        check = lambda res: bool(np.array_equal(res, p.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64))))
     elif c in ("v", "r", "vR", "rR", "vS", "rS", "u", "uR", "uo"):
         n = 100_000
         if c[0] == "v":

@@ -2,7 +2,8 @@
 workgroup (NWC), buffers per unit (UC, static ranges only), workgroups per CU
 (WGC), static ranges instead of stealing (STEAL=0), the shared part of a
 range (SSH: cnt >> SSH), counter spacing (SSTRIDE words), no stealing from other
-workgroups (NOSCAN=1), or the 160 KiB single-workgroup kernel (FULL=1).
+workgroups (NOSCAN=1), many shrinking workgroups in dispatch order (GUIDED=avg
+buffers per workgroup, with STEAL=0; EQUAL=1: equal sizes), or the 160 KiB single-workgroup kernel (FULL=1).
     NAME=c16u1 NWC=16 UC=1 python tools/diag/abl_compact.py
     NAME=full FULL=1 python tools/diag/abl_compact.py
 and then make -C nvlevelz_amd/csrc variant NAME=$NAME VSRC=$PWD/build/abl_$NAME.hip VFLAGS=-I$PWD/nvlevelz_amd/csrc"""
@@ -39,5 +40,10 @@ if os.environ.get("SSTRIDE"):
     rep("constexpr uint32_t kStealStride = 16;", "constexpr uint32_t kStealStride = %d;" % int(os.environ["SSTRIDE"]))
 if os.environ.get("NOSCAN"):
     rep("      const uint32_t v = *done ? kNoUnit : scan();", "      const uint32_t v = kNoUnit; (void)scan;")
+if os.environ.get("GUIDED"):  # dispatch-order ranges, GUIDED buffers per workgroup on average (STEAL=0)
+    rep("constexpr bool kCompactGuided = false;", "constexpr bool kCompactGuided = true;")
+    rep("constexpr uint32_t kGuidedAvg = 32;", "constexpr uint32_t kGuidedAvg = %d;" % int(os.environ["GUIDED"]))
+if os.environ.get("EQUAL"):
+    rep("constexpr bool kGuidedQuadratic = true;", "constexpr bool kGuidedQuadratic = false;")
 os.makedirs(os.path.join(R, "build"), exist_ok=True)
 open(os.path.join(R, "build", "abl_%s.hip" % os.environ["NAME"]), "w").write(s)

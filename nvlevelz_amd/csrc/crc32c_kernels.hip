@@ -2886,9 +2886,10 @@ __device__ const uint16_t* lpt_order(const VarGeom& g, uint8_t* lds, uint64_t i0
 __global__ __launch_bounds__(kWave * kGenWaves, 1) void crc32c_var_fused_kernel(VarGeom gv, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kFusedLdsBytes > kPermLdsBytes ? kFusedLdsBytes : kPermLdsBytes];
   if (ka.route.parts) {
-    uint64_t lo, hi;
-    if (route_region(ka.route, lo, hi)) return;  // the region path ran
-    const int rv = route_other(ka.route);
+    // the route kernel's verdict (written by its workgroup 0 before anything
+    // else; this launch follows it on the stream)
+    const int rv = (int)ldc(&ka.route.parts[kRoutePlanMax].bad, 0);
+    if (rv == kRouteRegion) return;  // the region path ran
     if (rv == kRoutePagesAligned) {  // every buffer one aligned 4 KiB chunk: config 2's loop over the list
       run_pairs<kFastU, kGenWaves, kAligned, VarGeom>(gv, ka, lds);  // (the kLdsBytes image: the region one
                                                                      // and this kernel's own LDS exceed 160 KiB)
@@ -3839,7 +3840,11 @@ __global__ __launch_bounds__(kPlanT) void crc32c_route_plan(const uint64_t* __re
 __global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg, VarGeom vg, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLdsBytes > kRLdsBytes ? kHeadLdsBytes : kRLdsBytes];
   uint64_t lo, hi;
+  // (workgroup 0 stores the verdict for the body kernel: one word after the
+  // partials, written in each branch so nothing extra stays live)
+  uint64_t* const verdict = &const_cast<RoutePart*>(ka.route.parts)[kRoutePlanMax].bad;
   if (route_region(ka.route, lo, hi)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *verdict = kRouteRegion;
     if (ka.route.dyn) {
       const uintptr_t base = (uintptr_t)ka.route.base, start = base + lo;
       const uintptr_t O = start & ~(uintptr_t)(kChunk - 1u);
@@ -3853,8 +3858,10 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg
     const uint32_t G = (uint32_t)max<uint64_t>(1u, min<uint64_t>(gridDim.x, gw));
     if (blockIdx.x >= G) return;
     run_region<kFastU>(rg, ka, lds, G);
-  } else if (route_other(ka.route) == kRouteHeads) {
-    if (blockIdx.x >= ka.tile_G) return;
+  } else {
+    const int kind = route_other(ka.route);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *verdict = (uint64_t)kind;
+    if (kind != kRouteHeads || blockIdx.x >= ka.tile_G) return;
     run_heads(vg, ka, lds);
   }  // (the page path runs in crc32c_var_fused_kernel: here its registers would spill the region path's SGPRs)
 }
@@ -4212,7 +4219,8 @@ static uint32_t next_generation() {
 }
 
 // Routed calls (crc32c_route_plan -> crc32c_route_kernel -> crc32c_var_fused_kernel).
-size_t route_parts_bytes() { return (dev::kRoutePlanMax * sizeof(dev::RoutePart) + 255u) / 256u * 256u; }
+// the plan's partials and, after them, the route kernel's verdict
+size_t route_parts_bytes() { return ((dev::kRoutePlanMax + 1u) * sizeof(dev::RoutePart) + 255u) / 256u * 256u; }
 // Region chunks a region-shaped batch_dev batch can span: sorted, each buffer
 // <= kRegionMaxLen (32 chunks), gaps <= 1/8 of the bytes + 64 KiB -> at most
 // 36 chunks per buffer + 18 + 2 (route_region checks it).

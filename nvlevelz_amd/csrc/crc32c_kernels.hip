@@ -244,8 +244,11 @@ __device__ __forceinline__ uint32_t shift4096(const uint8_t* lds, uint32_t acc, 
   return s;
 }
 
-// The same fill in two halves (loads, then stores), for a caller that issues
-// the blob's loads ahead of its first chunk loads (run_pairs).
+// The LDS image from the device table blob, in two halves: the loads (issued
+// ahead of a wave's first chunk loads, so the fill waits for the blob alone),
+// then the stores -- the replicated slice tables as 8192 16-byte slots
+// (consecutive lanes write consecutive 16 B: conflict-free ds_write_b128),
+// the comb + sh4096 operators (7168 words) verbatim, the work counter.
 template <int NW>
 struct LdsFill {
   uint32_t rep[(8192 + kWave * NW - 1) / (kWave * NW)];
@@ -284,30 +287,6 @@ __device__ __forceinline__ void fill_lds_store(uint8_t* lds, const LdsFill<NW>& 
   for (int q = 0; q < (1792 + kT - 1) / kT; ++q)
     if (t + q * kT < 1792) dst[t + q * kT] = f.op[q];
   if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = ctr0;
-}
-
-// Fill the LDS image from the device table blob.
-template <int NW>
-__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* __restrict__ g, uint32_t ctr0 = NW) {
-  constexpr int kT = kWave * NW;
-  const int t = threadIdx.x;
-  // replicated slice tables: 8192 16-byte stores, consecutive lanes write
-  // consecutive 16 B (conflict-free ds_write_b128).
-#pragma unroll
-  for (int q = 0; q < (8192 + kT - 1) / kT; ++q) {
-    const uint32_t s = (uint32_t)(t + q * kT);  // 16-byte slot index
-    if ((8192 % kT) != 0 && s >= 8192u) break;
-    const uint32_t off = s << 4;
-    const uint32_t tab = ((off >> 16) << 1) | ((off >> 7) & 1u);
-    const uint32_t b = (off >> 8) & 0xFFu;
-    const uint32_t v = g[kGSlice + tab * 256u + b];
-    *reinterpret_cast<uint4*>(lds + kSliceOff + off) = make_uint4(v, v, v, v);
-  }
-  // comb + sh4096 copied verbatim (7168 words = 1792 uint4)
-  const uint4* src = reinterpret_cast<const uint4*>(g + kGComb);
-  uint4* dst = reinterpret_cast<uint4*>(lds + kCombOff);
-  for (int q = t; q < 1792; q += kT) dst[q] = src[q];
-  if (t == 0) *reinterpret_cast<uint32_t*>(lds + kCtrOff) = ctr0;  // units 0..ctr0-1 are pre-assigned
 }
 
 __device__ __forceinline__ uint32_t finish(uint32_t crc, uint32_t flags) {

@@ -51,9 +51,15 @@ for it in range(int(os.environ.get("ITERS", "30"))):
     cnt = (s[:, 3] & 0xFFFFFFFF).astype(np.float64)
     busy = (s[:, 2] - s[:, 1]) / 100.0
     r["units_p10_p50_p90"] = [float(np.percentile(cnt, q)) for q in (10, 50, 90)]
+    wpg = int(os.environ.get("WAVES_PER_WG", "16"))
+    wge = end[: (len(end) // wpg) * wpg].reshape(-1, wpg).max(axis=1)  # each workgroup's last wave end
+    r["wg_end_mean_p10_p50_p90_max"] = [round(float(wge.mean()), 2)] + [round(float(np.percentile(wge, q)), 2)
+                                                                         for q in (10, 50, 90, 100)]
     r["units_total"] = int(cnt.sum())
     r["us_per_unit_p50"] = round(float(np.median(busy / np.maximum(cnt, 1))), 3)
     rows.append(r)
     print(json.dumps(r), flush=True)
 keys = ["event_us", "span_us", "outside_us", "start_spread_us", "fill_us_p50", "end_p50_us", "end_max_us"]
+print(json.dumps({"wg_end_median_of_launches": [round(float(np.median([r["wg_end_mean_p10_p50_p90_max"][k] for r in rows[2:]])), 2)
+                                                for k in range(5)]}))
 print(json.dumps({"median": {k: round(float(np.median([r[k] for r in rows[2:]])), 2) for k in keys}}))

@@ -324,3 +324,32 @@ def test_compact_image_lookups_and_banks():
                 assert len({(nad[l][n] // 4) % 32 for l in g}) == 32
     ctr = (128 * 256 + 128 + 31 * 4) // 4  # kCCtrOff: lane 63's slot, row (n=0, v=0, h=1)
     assert ctr == 128 * 64 + 32 + 31
+
+
+def test_region_long_fold_runs():
+    """The cooperative fold of a long region buffer (tools/diag/long_fold.patch,
+    measured and not shipped -- DESIGN §8 item 0): items
+    0..nit-1 (the head term, then the middle chunks' raws) split into 8
+    runs [ceil(nit q / 8), ceil(nit (q+1) / 8)) -- run 0 always holds item 0
+    --, each run's Horner times x^(8*4096*(nit - end + 1)), XORed, equals the
+    per-lane chain acc = shift4096(acc) ^ item, shifted once more (fold_out's
+    longer branch)."""
+    rng = random.Random(11)
+    for nit in list(range(2, 34)) + [40, 63]:
+        items = [rng.getrandbits(32) for _ in range(nit)]
+        acc = items[0]
+        for t in range(1, nit):
+            acc = km.shift(acc, 4096) ^ items[t]
+        acc = km.shift(acc, 4096)
+        got = 0
+        for q in range(8):
+            a, b = (nit * q + 7) // 8, (nit * (q + 1) + 7) // 8
+            if q == 0:
+                assert a == 0 and b >= 1
+            if b <= a:
+                continue
+            P = items[a]
+            for t in range(a + 1, b):
+                P = km.shift(P, 4096) ^ items[t]
+            got ^= km.shift(P, 4096 * (nit - b + 1))
+        assert got == acc, nit

@@ -27,6 +27,7 @@ lib.nvl_diag_stamps.restype = ctypes.c_int
 NWV = int(os.environ.get("NWAVES", "4096"))  # waves of the launch (compact kernel: 512 x 12 or 16)
 h = np.zeros(4 * NWV, dtype=np.uint64)
 rows = []
+wg_ends = []  # per launch: each workgroup's last-wave end minus the launch's mean
 for it in range(int(os.environ.get("ITERS", "30"))):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -55,11 +56,20 @@ for it in range(int(os.environ.get("ITERS", "30"))):
     wge = end[: (len(end) // wpg) * wpg].reshape(-1, wpg).max(axis=1)  # each workgroup's last wave end
     r["wg_end_mean_p10_p50_p90_max"] = [round(float(wge.mean()), 2)] + [round(float(np.percentile(wge, q)), 2)
                                                                          for q in (10, 50, 90, 100)]
+    wg_ends.append(wge - wge.mean())  # each workgroup's lateness in this launch
     r["units_total"] = int(cnt.sum())
     r["us_per_unit_p50"] = round(float(np.median(busy / np.maximum(cnt, 1))), 3)
     rows.append(r)
     print(json.dumps(r), flush=True)
 keys = ["event_us", "span_us", "outside_us", "start_spread_us", "fill_us_p50", "end_p50_us", "end_max_us"]
+if len(wg_ends) > 4:  # is a workgroup's lateness persistent from one launch to the next?
+    W = np.array(wg_ends[2:])
+    cc = [float(np.corrcoef(W[k], W[k + 1])[0, 1]) for k in range(len(W) - 1)]
+    mean_late = W.mean(axis=0)
+    print(json.dumps({"wg_lateness_corr_consecutive_launches": [round(c, 3) for c in cc[:8]],
+                      "corr_median": round(float(np.median(cc)), 3),
+                      "std_per_launch_us": round(float(W.std(axis=1).mean()), 2),
+                      "std_of_mean_over_launches_us": round(float(mean_late.std()), 2)}))
 print(json.dumps({"wg_end_median_of_launches": [round(float(np.median([r["wg_end_mean_p10_p50_p90_max"][k] for r in rows[2:]])), 2)
                                                 for k in range(5)]}))
 print(json.dumps({"median": {k: round(float(np.median([r[k] for r in rows[2:]])), 2) for k in keys}}))

@@ -2304,6 +2304,16 @@ constexpr int kGenPairU = 2;   // buffers per unit (g: 67.7 us at 2, 70.4 at 1, 
 template <int M>
 constexpr int waves_of() { return M == kGeneral ? kGenWaves : kWavesPerWG; }
 
+// Aligned one-chunk batches of at least kLongFixedMin blocks (config 5's
+// whole-rank step) run this copy of crc32c_fixed_kernel<kAligned>'s J == 1
+// path: the same code under its own name, so a profile's per-kernel
+// statistics keep config 2-sized launches (~64 us) apart from ms-long ones.
+constexpr uint64_t kLongFixedMin = 1ull << 18;
+__global__ __launch_bounds__(kThreads, 1) void crc32c_fixed_long_kernel(FixedGeom g, KArgs ka) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes > kRLdsBytes ? kLdsBytes : kRLdsBytes];
+  run_pairs<kFastU, kWavesPerWG, kAligned, FixedGeom, false, true>(g, ka, lds);
+}
+
 template <int M>
 __global__ __launch_bounds__(kWave * waves_of<M>(), 1) void crc32c_fixed_kernel(FixedGeom g, KArgs ka) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes > kRLdsBytes ? kLdsBytes : kRLdsBytes];
@@ -4090,6 +4100,14 @@ hipError_t launch_fixed(const LaunchCtx& lc, const uint8_t* base, uint64_t strid
   dev::KArgs ka{out, flags, recs, lc.tables, nullptr, hc};
   hipEvent_t stop_main = J == 1 ? lc.ev_stop : nullptr;  // else the fix-up records it
   const bool timed = ev_start || stop_main;
+  if (aligned && J == 1 && n >= dev::kLongFixedMin) {
+    if (timed)
+      hipExtLaunchKernelGGL(dev::crc32c_fixed_long_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, ev_start,
+                            stop_main, 0u, g, ka);
+    else
+      hipLaunchKernelGGL(dev::crc32c_fixed_long_kernel, dim3(grid), dim3(dev::kThreads), 0, lc.stream, g, ka);
+    return hipGetLastError();
+  }
   if (aligned) {
     if (timed)
       hipExtLaunchKernelGGL(dev::crc32c_fixed_kernel<dev::kAligned>, dim3(grid), dim3(dev::kThreads), 0, lc.stream,

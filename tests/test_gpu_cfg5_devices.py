@@ -78,6 +78,25 @@ def test_config5_full_one_gpu(dev, C, port):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("mask,init", [(False, 0), (True, 0x1234ABCD)])
+def test_fixed_long_kernel_threshold(dev, C, port, mask, init):
+    """Aligned 4 KiB batches of >= 2^18 blocks run crc32c_fixed_long_kernel
+    (launch_fixed); one block fewer runs crc32c_fixed_kernel<kAligned>.  Both
+    sides of the threshold agree block for block, and a sample with the oracle."""
+    L, n = 4096, 1 << 18
+    buf = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    C.fill_splitmix(buf, n, L, 0x5EED0005)
+    long_ = _u32(C.extend_fixed(buf, L, L, n, init, mask=mask))
+    short = _u32(C.extend_fixed(buf, L, L, n - 1, init, mask=mask))
+    assert np.array_equal(long_[:n - 1], short)
+    idx = np.array([0, 1, 4095, 4096, n // 2, n - 2, n - 1])
+    sample = buf.view(n, L)[torch.from_numpy(idx).to(dev)].cpu().numpy().reshape(-1)
+    want = port.fixed(sample, L, L, idx.size, np.full(idx.size, init, dtype=np.uint32))
+    if mask:
+        want = np.array([port.mask(int(x)) for x in want], dtype=np.uint32)
+    assert np.array_equal(long_[idx], want)
+
+
 def test_fixed_dev_timed_matches_and_times(dev, C):
     n, L = 20000, 4096
     buf = torch.empty(n * L, dtype=torch.uint8, device=dev)

@@ -40,7 +40,7 @@ def usage(tmp_path_factory):
     return kernels
 
 
-HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_var_kernel", "crc32c_var_fused_kernel",
+HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_fixed_long_kernel", "crc32c_var_kernel", "crc32c_var_fused_kernel",
        "crc32c_region_kernel", "crc32c_chunks_kernel",
        "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel", "crc32c_route_kernel", "crc32c_route_plan"]
 # SGPR spills go to VGPR lanes (v_writelane/v_readlane), not memory: a bound

@@ -443,7 +443,21 @@ def cfg5_leg(steps: int, warmup: int, rank: int, world: int, dev, red_dev, golde
             "period_us_per_step_rank0": round(period_s * 1e6, 2),
             "frac_what": "rank 0's alg bytes (its blocks x (4096 + 4)) / its period per step (HIP events around the "
                          "timed steps / steps) / 8 TB/s; frac_min_over_ranks the slowest rank's",
+            "traffic_over_alg": _cfg5_traffic(n_local),
             "verify": v}
+
+
+def _cfg5_traffic(n_local: int):
+    """Committed PMC (not measured in this run): HBM bytes / algorithmic bytes
+    of crc32c_fixed_long_kernel over config 5's one-GPU batch
+    (profiles/r05_pmc_cfg5_long.json, tools/pmc.sh + tools/pmc_workloads.py);
+    None for any other per-rank batch."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r05_pmc_cfg5_long.json")) as f:
+            w = json.load(f)["workloads"]["cfg5_one_gpu"]
+        return w["traffic_over_alg"] if w["alg_bytes"] == n_local * (BLOCK + 4) else None
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def main():

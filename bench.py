@@ -408,26 +408,15 @@ def cfg5_leg(steps: int, warmup: int, rank: int, world: int, dev, red_dev, golde
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    period_s = ev0.elapsed_time(ev1) / 1e3 / steps
+    # each rank's own window (shard.timed_window: the closing barrier outside
+    # `elapsed`), then the slowest rank's
+    tw = shard.timed_window(step, steps, stream=stream, world=world)
+    period_s = tw["period_s"]
     frac = n_local * (BLOCK + 4) / period_s / 1e9 / HBM_PEAK_GBS
-    frac_min = frac
-    if world > 1:
-        t = torch.tensor([elapsed, -frac], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, frac_min = float(t[0].item()), -float(t[1].item())
+    rows = shard.gather_floats([tw["elapsed_s"], period_s, tw["barrier_after_s"], n_local], red_dev)
+    elapsed = float(rows[:, 0].max())
+    frac_r = rows[:, 3] * (BLOCK + 4) / rows[:, 1] / 1e9 / HBM_PEAK_GBS
+    frac_min = float(frac_r.min())
     nb = len(batches)
     del batches, buf, out
     torch.cuda.empty_cache()
@@ -443,8 +432,24 @@ def cfg5_leg(steps: int, warmup: int, rank: int, world: int, dev, red_dev, golde
             "period_us_per_step_rank0": round(period_s * 1e6, 2),
             "frac_what": "rank 0's alg bytes (its blocks x (4096 + 4)) / its period per step (HIP events around the "
                          "timed steps / steps) / 8 TB/s; frac_min_over_ranks the slowest rank's",
+            "timing_what": "value = all blocks x steps / the MAX over ranks of each rank's own elapsed (its start "
+                           "after the opening barrier + synchronize to its own synchronize after the last launch; "
+                           "the closing barrier is timed apart, barrier_after_ms)",
+            "per_rank": _per_rank(rows),
             "traffic_over_alg": _cfg5_traffic(n_local),
             "verify": v}
+
+
+def _per_rank(rows) -> list:
+    """Rows of shard.gather_floats([elapsed_s, period_s, barrier_after_s,
+    blocks]) -> one object per rank: its own wall window, its kernel period
+    (HIP events on its launch stream) and that period's roofline fraction."""
+    out = []
+    for r, (el, per, bar, nb) in enumerate(rows):
+        out.append({"rank": r, "elapsed_ms": round(el * 1e3, 4), "period_us": round(per * 1e6, 2),
+                    "frac": round(nb * (BLOCK + 4) / per / 1e9 / HBM_PEAK_GBS, 4),
+                    "barrier_after_ms": round(bar * 1e3, 4), "blocks": int(nb)})
+    return out
 
 
 def _cfg5_traffic(n_local: int):
@@ -559,20 +564,9 @@ def main():
     # events on the launch stream bracket the region (interval / K = mean
     # launch period, gaps included).
     K = args.steps
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(K):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    region_ms = ev0.elapsed_time(ev1)
+    tw = shard.timed_window(step, K, stream=stream, world=world)
+    elapsed = tw["elapsed_s"]
+    region_ms = tw["period_s"] * K * 1e3
     # Beside the in-regime figure, two untimed diagnostic passes (K launches
     # each, after the timed region; tools/rocprof_summary.py splits them off a
     # rocprofv3 trace of this command by launch order):
@@ -632,15 +626,12 @@ def main():
         pe[1].record(stream)
         torch.cuda.synchronize()
         probe = {"bytes": nb, "period_us": pe[0].elapsed_time(pe[1]) * 1e3 / args.probe}
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        nt = torch.tensor([n_local], dtype=torch.int64, device=red_dev)
-        dist.all_reduce(nt, op=dist.ReduceOp.SUM)
-        total_blocks = int(nt.item())
-    else:
-        total_blocks = n_local
+    # the slowest rank's own window (each rank's elapsed ends at its own
+    # synchronize; the closing barrier is timed apart) and every rank's period
+    rows = shard.gather_floats([elapsed, tw["period_s"], tw["barrier_after_s"], n_local], red_dev)
+    own_elapsed = elapsed
+    elapsed = float(rows[:, 0].max())
+    total_blocks = int(round(rows[:, 3].sum()))
 
     value = total_blocks * BLOCK * K / elapsed / 2**30
     # Roofline: the kernel's average launch duration in the timed region
@@ -650,7 +641,7 @@ def main():
     # the kernel's fraction) and can never exceed the wall-clock step.
     period_s = region_ms / 1e3 / K
     step_s = elapsed / K
-    assert period_s <= step_s * 1.0001, (period_s, step_s)  # events inside the wall-clock bracket
+    assert period_s <= own_elapsed / K * 1.0001, (period_s, own_elapsed / K)  # events inside the wall-clock bracket
     alg_bytes = n_local * (BLOCK + 4)  # every input byte once + 4 B CRC out
     achieved = alg_bytes / period_s / 1e9
     frac = achieved / HBM_PEAK_GBS
@@ -735,6 +726,12 @@ def main():
                          "isolated_frac": round(alg_bytes / (float(np.median(iso_ms)) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                          "isolated_what": "untimed diagnostic: ordinary events before and after each launch (the "
                                           "launch starts from an idle queue, as a single shim call does); median"},
+            "timing": {"what": "value = all ranks' blocks x K / the MAX over ranks of each rank's own elapsed "
+                               "(from its start after the opening barrier + synchronize to its own synchronize "
+                               "after the K launches); the closing barrier is outside it (barrier_after_ms); "
+                               "per_rank: each rank's window, its kernel period (HIP events on its launch "
+                               "stream / K) and that period's roofline fraction",
+                       "per_rank": _per_rank(rows)},
             "cpu_baseline": cpu,
             "verify": verify,
         }

@@ -11,6 +11,9 @@ from __future__ import annotations
 
 import numpy as np
 
+# (timed_window / gather_floats: bench.py's per-rank timing, SURVEY §8e "wall
+# time from the first launch to the last completion" -- the slowest rank's)
+
 
 def local_count(n_total: int, rank: int, world: int) -> int:
     """Number of round-robin blocks rank owns out of n_total."""
@@ -88,6 +91,66 @@ def verify_local(crcs: np.ndarray, expect: dict) -> dict:
     if "crc_last" in expect and crcs.size:
         out["crc_last_ok"] = int(crcs[-1]) == expect["crc_last"]
     return out
+
+
+def timed_window(launch, steps: int, *, stream=None, world: int = 1, sync=None, group=None) -> dict:
+    """One rank's timed region (bench.py's contract: barrier + synchronize on
+    both sides of exactly `steps` launches).  Returns this rank's own
+    `elapsed_s` -- from its start (after the opening barrier and
+    synchronize) to its own synchronize after the last launch -- and, apart
+    from it, `barrier_after_s`: the time this rank then waits in the closing
+    barrier for the slowest rank.  The closing barrier stays outside
+    `elapsed_s`, so the max over ranks of `elapsed_s` (max_over_ranks) is the
+    slowest rank's own time, not that time plus an RCCL barrier's latency and
+    the other ranks' skew (the 20-launch windows are
+    ~1.3 ms, where a barrier's tens of µs read as a false efficiency loss).
+    With `stream`, two HIP events on it bracket the launches: `period_s` =
+    their interval / steps (the per-rank kernel period).  `sync` (default
+    torch.cuda.synchronize) lets CPU tests time host-side work."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    if sync is None:
+        sync = torch.cuda.synchronize
+    ev = None
+    if stream is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if world > 1:
+        dist.barrier(group=group)
+    sync()
+    t0 = time.perf_counter()
+    if ev:
+        ev[0].record(stream)
+    for _ in range(steps):
+        launch()
+    if ev:
+        ev[1].record(stream)
+    sync()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier(group=group)
+    t2 = time.perf_counter()
+    out = {"elapsed_s": t1 - t0, "barrier_after_s": t2 - t1, "period_s": None}
+    if ev:
+        out["period_s"] = ev[0].elapsed_time(ev[1]) / 1e3 / max(steps, 1)
+    return out
+
+
+def gather_floats(vals, device, group=None) -> np.ndarray:
+    """All-gather a short float vector from every rank: row r = rank r's
+    (float64; one all_gather, outside any timed region).  Without a process
+    group, the one row."""
+    import torch
+    import torch.distributed as dist
+
+    v = torch.tensor([float(x) for x in vals], dtype=torch.float64, device=device)
+    if not (dist.is_available() and dist.is_initialized()):
+        return v.cpu().numpy()[None, :]
+    outs = [torch.empty_like(v) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(outs, v, group=group)
+    return torch.stack(outs).cpu().numpy()
 
 
 def verify_shards(local, n_total: int, expect: dict, group=None) -> dict:

@@ -282,3 +282,56 @@ def test_launch_module_loads_no_hip():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert r.stdout.split() == ["1", "False", "False"], r.stdout
+
+
+def _window_worker(rank, world, port, result_q):
+    """bench.py's timed region on the CPU (shard.timed_window, gloo): rank 1's
+    launches take 60 ms each, rank 0's 1 ms, so rank 0 finishes early and
+    waits in the closing barrier."""
+    import torch.distributed as dist
+    from nvlevelz_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dt = 0.060 if rank == 1 else 0.001
+        tw = shard.timed_window(lambda: time.sleep(dt), 4, world=world, sync=lambda: None)
+        rows = shard.gather_floats([tw["elapsed_s"], 1.0, tw["barrier_after_s"], 10], torch.device("cpu"))
+        result_q.put((rank, tw, rows.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_timed_window_keeps_the_closing_barrier_outside_elapsed():
+    """each rank's `elapsed` ends at its own synchronize;
+    the wait for the slowest rank is reported apart (barrier_after_s), and the
+    line's time is the max over ranks of the ranks' own windows."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_window_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = {r: (tw, rows) for r, tw, rows in (q.get(timeout=120) for _ in range(2))}
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    tw0, rows = res[0]
+    tw1, _ = res[1]
+    assert tw0["period_s"] is None  # no stream: no events
+    assert tw0["elapsed_s"] < 0.1, tw0          # 4 x 1 ms of its own work
+    assert tw0["barrier_after_s"] > 0.1, tw0    # then waits ~240 ms for rank 1, outside elapsed
+    assert 0.23 < tw1["elapsed_s"] < 1.0, tw1
+    assert res[1][1] == rows                    # every rank holds every rank's row
+    assert max(r[0] for r in rows) == tw1["elapsed_s"]
+    assert [r[3] for r in rows] == [10.0, 10.0]
+
+
+def test_timed_window_single_rank():
+    from nvlevelz_amd import shard
+    calls = []
+    tw = shard.timed_window(lambda: calls.append(1), 5, sync=lambda: None)
+    assert len(calls) == 5 and tw["barrier_after_s"] < 0.01 and tw["period_s"] is None
+    rows = shard.gather_floats([tw["elapsed_s"], 2.0], torch.device("cpu"))
+    assert rows.shape == (1, 2) and rows[0, 1] == 2.0

@@ -208,6 +208,7 @@ def cpu_baseline(host: np.ndarray, n: int, seconds: float, threads: int, reps: i
         "value": round(gibs_all, 3), "unit": "GiB/s", "cores": int(round(par_all)), "kind": kind,
         "threads": th, "effective_parallelism": round(par_all, 2),
         "per_thread_gibs": round(gibs_all / max(par_all, 1e-9), 3),
+        "cpu_s_per_GiB": round(par_all / gibs_all, 4),
         "sample": f"median of {reps} repetitions x {passes_all} passes over the first {n} x 4 KiB blocks of this "
                   f"rank's batch ({th} threads = the physical cores of the {logical} CPUs in this process's "
                   f"affinity set ({phys}) capped by the cgroup quota ({quota} CPUs), contiguous share per thread; "
@@ -676,14 +677,21 @@ def main():
         pinned.copy_(buf[:ne * BLOCK].cpu())
         hp = pinned.numpy()
         crc32c.extend_fixed_host(hp, BLOCK, BLOCK, ne)
+        import resource
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t1 = time.perf_counter()
         reps = 5
         for _ in range(reps):
             r = crc32c.extend_fixed_host(hp, BLOCK, BLOCK, ne)
         el = time.perf_counter() - t1
-        e2e = {"value": round(ne * BLOCK * reps / el / 2**30, 3), "unit": "GiB/s",
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        gib = ne * BLOCK * reps / 2**30
+        e2e = {"value": round(gib / el, 3), "unit": "GiB/s",
                "what": f"{ne} x 4 KiB pinned host blocks -> H2D -> kernel -> D2H of u32 results "
                        f"(nvl_crc32c_fixed_host, 2-stream pipeline, synchronous), {reps} calls",
+               "host_cpu_s_per_GiB": round(((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / gib, 4),
+               "host_cpu_what": "getrusage user + sys of every thread of this process over the calls / GiB "
+                                "checksummed (the reference CPU leg: cpu_baseline.cpu_s_per_GiB)",
                "ok": bool(np.array_equal(r, res[:ne]))}
 
     if rank == 0:

@@ -210,8 +210,11 @@ NVL_API int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengt
 /* Host region variant: n buffers that all lie inside ONE host region
  * [region, region + region_len) (a file image, a log block run): buffer i is
  * region[offsets[i] .. offsets[i]+lengths[i]).  The covered range is staged
- * once (one pinned copy, one H2D), then batched as nvl_crc32c_batch_dev.
- * Synchronous. */
+ * once (one pinned copy, one H2D; none when it lies in a range registered
+ * with nvl_crc32c_host_register: DMA from the caller's pages, or with
+ * NVL_CRC32C_FLAG_HOST_ZERO_COPY no copy at all), then batched as
+ * nvl_crc32c_batch_dev.  Synchronous.  NVL_CRC32C_FLAG_HOST_ZERO_COPY on a
+ * range that is not registered: NVL_CRC32C_EINVAL. */
 NVL_API int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const uint64_t* offsets,
                                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all,
                                          uint32_t* out, uint64_t n, uint32_t flags);
@@ -236,6 +239,29 @@ NVL_API int nvl_crc32c_batch_region_host_multi(const void* region, uint64_t regi
  * returns the number of parts (>= 1), or a negative status. */
 NVL_API int nvl_crc32c_multi_plan(const uint64_t* offsets, const uint64_t* lengths, uint64_t n, int ndev,
                                   uint64_t min_bytes, uint64_t* part_first);
+
+/* ---- registered host memory: the staging-free host-resident path -------- */
+/* The fork's host-resident call sites start in pageable memory -- an mmap'd
+ * table (util/env_posix.cc:199-209), a TableBuilder's block buffer
+ * (table/table_builder.cc:185-187), a compaction's output -- which the
+ * host-resident entry points otherwise first copy into pinned staging on
+ * the calling CPU threads.  nvl_crc32c_host_register pins and maps
+ * [ptr, ptr + bytes) for every device (hipHostRegister, portable | mapped),
+ * once, for as long as the caller keeps it (e.g. the life of an mmap):
+ * nvl_crc32c_batch_region_host (and the _multi form, per device) then DMA a
+ * window that lies inside one registration straight from the caller's pages
+ * -- no CPU copy -- and with NVL_CRC32C_FLAG_HOST_ZERO_COPY run the kernels
+ * on the mapped pages themselves (they read over PCIe; nothing is copied to
+ * HBM).  Anything else (unregistered, or a window crossing a registration's
+ * end) still takes the pinned staging; a failed registration leaves the
+ * range unregistered and returns its status.  Registrations may not
+ * overlap (NVL_CRC32C_EINVAL).  nvl_crc32c_host_unregister takes the `ptr`
+ * that was registered; no call may be using the range. */
+#define NVL_CRC32C_FLAG_HOST_ZERO_COPY 0x4u /* host region entry: read registered pages in place */
+NVL_API int nvl_crc32c_host_register(const void* ptr, size_t bytes);
+NVL_API int nvl_crc32c_host_unregister(const void* ptr);
+/* 1 if [ptr, ptr + bytes) lies inside one registration, else 0. */
+NVL_API int nvl_crc32c_host_registered(const void* ptr, size_t bytes);
 
 /* Host fixed-stride batch (one contiguous host region, e.g. an mmap'd table
  * file or a pinned bench buffer), pipelined H2D/compute/D2H over two

@@ -26,6 +26,7 @@ ESELFTEST = -4
 ENOSPC = -5
 FLAG_MASK = 0x1
 FLAG_REGION_SHAPED = 0x2  # nvl_crc32c_region_dev: the caller checked the layout (one launch)
+FLAG_HOST_ZERO_COPY = 0x4  # host region entry: kernels read the registered pages in place
 REGION_MAX_LEN = 128 << 10
 
 _c = ctypes
@@ -63,6 +64,9 @@ SIGNATURES = {
     "nvl_crc32c_region_dev_timed": (_int, [_vp, _u64, _vp, _vp, _vp, _u32, _vp, _u64, _u32, _vp, _sz, _vp, _vp,
                                            _vp]),
     "nvl_crc32c_region_workspace_bytes": (_sz, [_u64, _u64]),
+    "nvl_crc32c_host_register": (_int, [_vp, _sz]),
+    "nvl_crc32c_host_unregister": (_int, [_vp]),
+    "nvl_crc32c_host_registered": (_int, [_vp, _sz]),
     # include/nvl_framing.h
     "nvl_framing_gpu_min_bytes": (_u64, []),
     "nvl_framing_uses_gpu": (_int, [_u64, _u32]),

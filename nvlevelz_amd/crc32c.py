@@ -332,13 +332,36 @@ def extend_fixed_host(buf: np.ndarray, stride: int, length: int, n: int, init=0,
     return out
 
 
+def host_register(arr) -> None:
+    """nvl_crc32c_host_register over a host array's bytes (numpy array or
+    buffer): pinned and mapped for every device until host_unregister, so
+    extend_region_host DMAs straight from it (no staging copy) or, with
+    ``zero_copy=True``, reads it in place.  The caller keeps ``arr`` alive."""
+    a = arr if isinstance(arr, np.ndarray) else np.frombuffer(arr, dtype=np.uint8)
+    check(lib.nvl_crc32c_host_register(a.ctypes.data, a.nbytes), "nvl_crc32c_host_register")
+
+
+def host_unregister(arr) -> None:
+    a = arr if isinstance(arr, np.ndarray) else np.frombuffer(arr, dtype=np.uint8)
+    check(lib.nvl_crc32c_host_unregister(a.ctypes.data), "nvl_crc32c_host_unregister")
+
+
+def host_registered(arr) -> bool:
+    a = arr if isinstance(arr, np.ndarray) else np.frombuffer(arr, dtype=np.uint8)
+    return lib.nvl_crc32c_host_registered(a.ctypes.data, a.nbytes) == 1
+
+
 def extend_region_host(region: np.ndarray, offsets, lengths, init=0, *, mask: bool = False,
-                       devices: Optional[Sequence[int]] = None, min_bytes_per_device: int = 0) -> np.ndarray:
+                       devices: Optional[Sequence[int]] = None, min_bytes_per_device: int = 0,
+                       zero_copy: bool = False) -> np.ndarray:
     """out[i] = Extend(init_i, region[offsets[i] : offsets[i] + lengths[i]]) for
     buffers in ONE host region (an mmap'd file image, a log block run):
     nvl_crc32c_batch_region_host on the current device, or with ``devices``
     nvl_crc32c_batch_region_host_multi -- contiguous ranges of the batch on
-    those devices at once, each over its own PCIe link (synchronous)."""
+    those devices at once, each over its own PCIe link (synchronous).  A
+    region inside a host_register()ed range is DMA'd from its own pages (no
+    staging copy); ``zero_copy`` (registered ranges only) has the kernels read
+    it in place over PCIe."""
     a = region if isinstance(region, np.ndarray) else np.frombuffer(region, dtype=np.uint8)
     a = np.ascontiguousarray(a).view(np.uint8)
     o = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -353,7 +376,7 @@ def extend_region_host(region: np.ndarray, offsets, lengths, init=0, *, mask: bo
     else:
         ini = np.ascontiguousarray(np.asarray(init, dtype=np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
         init_ptr = ini.ctypes.data
-    flags = FLAG_MASK if mask else 0
+    flags = (FLAG_MASK if mask else 0) | (_lib.FLAG_HOST_ZERO_COPY if zero_copy else 0)
     if devices is None:
         rc = lib.nvl_crc32c_batch_region_host(a.ctypes.data, a.nbytes, o.ctypes.data, m.ctypes.data, init_ptr,
                                               init_all, out.ctypes.data, n, flags)
@@ -397,5 +420,5 @@ def to_u32(t) -> np.ndarray:
 
 __all__ = ["extend", "value", "mask", "unmask", "kMaskDelta", "init", "gpu_accelerated",
            "extend_fixed", "FixedBatch", "extend_batch", "extend_region", "extend_batch_host", "extend_fixed_host",
-           "extend_region_host", "multi_plan", "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix",
+           "extend_region_host", "host_register", "host_unregister", "host_registered", "multi_plan", "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix",
            "to_u32", "Crc32cError"]

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -851,11 +852,67 @@ static hipError_t stage_h2d(uint8_t* dst, uint8_t* hst, const uint8_t* src, uint
   return e;
 }
 
+// ---- registered host ranges (nvl_crc32c_host_register) ---------------------
+// base -> bytes of every live registration (hipHostRegister, portable |
+// mapped: every device may DMA from it and map it).
+namespace {
+std::mutex g_reg_mu;
+std::map<uintptr_t, uint64_t> g_reg;
+
+// The registration holding [p, p + bytes), or g_reg.end(); caller holds g_reg_mu.
+std::map<uintptr_t, uint64_t>::const_iterator reg_find(uintptr_t p, uint64_t bytes) {
+  auto it = g_reg.upper_bound(p);
+  if (it == g_reg.begin()) return g_reg.end();
+  --it;
+  return (p >= it->first && bytes <= it->second && p - it->first <= it->second - bytes) ? it : g_reg.end();
+}
+}  // namespace
+
+int nvl_crc32c_host_register(const void* ptr, size_t bytes) {
+  if (!ptr || bytes == 0 || bytes > (1ull << 50)) return NVL_CRC32C_EINVAL;
+  const uintptr_t p = reinterpret_cast<uintptr_t>(ptr);
+  if (p + bytes < p) return NVL_CRC32C_EINVAL;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto nx = g_reg.lower_bound(p);
+  if (nx != g_reg.end() && nx->first < p + bytes) return NVL_CRC32C_EINVAL;  // overlaps a later one
+  if (nx != g_reg.begin()) {
+    auto pv = std::prev(nx);
+    if (pv->first + pv->second > p) return NVL_CRC32C_EINVAL;  // overlaps an earlier one
+  }
+  int rc = NVL_CRC32C_OK;
+  if (!current_state(&rc)) return rc;  // (a device and its runtime first: no GPU -> ENODEV)
+  if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterPortable | hipHostRegisterMapped) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return NVL_CRC32C_EHIP;
+  }
+  g_reg.emplace(p, (uint64_t)bytes);
+  return NVL_CRC32C_OK;
+}
+
+int nvl_crc32c_host_unregister(const void* ptr) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
+  if (!ptr || it == g_reg.end()) return NVL_CRC32C_EINVAL;
+  g_reg.erase(it);
+  if (hipHostUnregister(const_cast<void*>(ptr)) != hipSuccess) {
+    (void)hipGetLastError();
+    return NVL_CRC32C_EHIP;
+  }
+  return NVL_CRC32C_OK;
+}
+
+int nvl_crc32c_host_registered(const void* ptr, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  return ptr && reg_find(reinterpret_cast<uintptr_t>(ptr), bytes) != g_reg.end() ? 1 : 0;
+}
+
 int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const uint64_t* offsets,
                                  const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
                                  uint64_t n, uint32_t flags) {
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out || (!region && region_len)) return NVL_CRC32C_EINVAL;
+  if (flags & ~(NVL_CRC32C_FLAG_MASK | NVL_CRC32C_FLAG_HOST_ZERO_COPY)) return NVL_CRC32C_EINVAL;
   uint64_t lo = UINT64_MAX, hi = 0, max_len = 0;  // staged window [lo, hi)
   for (uint64_t i = 0; i < n; ++i) {
     if (lengths[i] > region_len || offsets[i] > region_len - lengths[i]) return NVL_CRC32C_EINVAL;
@@ -863,12 +920,33 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     if (offsets[i] + lengths[i] > hi) hi = offsets[i] + lengths[i];
     max_len = std::max(max_len, lengths[i]);
   }
+  const uint64_t wbytes = hi - lo;
+  const uint8_t* src = static_cast<const uint8_t*>(region) + lo;
+  // A window inside one registration (nvl_crc32c_host_register): DMA from the
+  // caller's pages (no staging copy), or with ZERO_COPY no copy at all.
+  const bool reg = nvl_crc32c_host_registered(src, wbytes) == 1;
+  const bool zero_copy = (flags & NVL_CRC32C_FLAG_HOST_ZERO_COPY) != 0;
+  if (zero_copy && !reg) return NVL_CRC32C_EINVAL;
+  flags &= NVL_CRC32C_FLAG_MASK;
   int rc = NVL_CRC32C_OK;
   DeviceState* s = current_state(&rc);
   if (!s) return rc;
-  // host layout: [window bytes] [offsets n (rebased to the window)] [lengths n] [init n]
-  const uint64_t wbytes = hi - lo;
-  const size_t meta_off = align_up(wbytes, 256);
+  const uint8_t* dsrc = nullptr;  // the kernels' view of the window (zero copy)
+  if (zero_copy) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, const_cast<uint8_t*>(src), 0) != hipSuccess || !dp) {
+      (void)hipGetLastError();
+      return NVL_CRC32C_EHIP;
+    }
+    dsrc = static_cast<const uint8_t*>(dp);
+    // The kernels read whole 4 KiB pages of the window (the region grid from
+    // the page below its start; the batch kernels within the buffers' own
+    // pages): safe only if the device view keeps the host page offsets, so
+    // that every page read holds a registered byte.
+    if (((uintptr_t)dsrc & 4095u) != ((uintptr_t)src & 4095u)) return NVL_CRC32C_EHIP;
+  }
+  // host layout: [window bytes (staged calls only)] [offsets n (rebased to the window)] [lengths n] [init n]
+  const size_t meta_off = reg ? 0 : align_up(wbytes, 256);
   const size_t total = meta_off + n * 8 * 2 + n * 4 + 256;
   uint8_t* hst = static_cast<uint8_t*>(t_res.staging.get(total));
   if (!hst) return NVL_CRC32C_EHIP;
@@ -879,14 +957,23 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
   // otherwise the batch path with the host's bound on the lengths
   const bool as_region = max_len <= kRegionMaxLen && region_sorted(offsets, lengths, n);
   const size_t ws = as_region ? region_ws_bytes(wbytes, n) : batch_ws(n, s->num_cu, 0).total;
-  const size_t dbytes = align_up(total, 256) + align_up(n * 4, 256) + ws + 256;
+  // device layout: [window (not for zero copy)] [metadata] [out] [workspace]
+  const size_t win_dev = zero_copy ? 0 : align_up(wbytes, 256);
+  const size_t dbytes = win_dev + align_up(total - meta_off, 256) + align_up(n * 4, 256) + ws + 256;
   if (hipMallocAsync(&d, dbytes, st) != hipSuccess) return NVL_CRC32C_EHIP;
-  uint32_t* dout = reinterpret_cast<uint32_t*>(d + align_up(total, 256));
-  void* dws = d + align_up(total, 256) + align_up(n * 4, 256);
-  // The window goes to the GPU in slices: the staging copy of slice k+1 (a
-  // few host threads for large windows) overlaps the H2D DMA of slice k, so
-  // the call costs max(copy, PCIe) instead of their sum.
-  hipError_t e = stage_h2d(d, hst, static_cast<const uint8_t*>(region) + lo, wbytes, st);
+  uint8_t* dmeta = d + win_dev;
+  uint32_t* dout = reinterpret_cast<uint32_t*>(dmeta + align_up(total - meta_off, 256));
+  void* dws = reinterpret_cast<uint8_t*>(dout) + align_up(n * 4, 256);
+  const uint8_t* dwin = zero_copy ? dsrc : d;
+  hipError_t e = hipSuccess;
+  if (reg && !zero_copy && wbytes) {
+    e = hipMemcpyAsync(d, src, wbytes, hipMemcpyHostToDevice, st);  // DMA from the registered pages
+  } else if (!reg) {
+    // The window goes to the GPU in slices: the staging copy of slice k+1 (a
+    // few host threads for large windows) overlaps the H2D DMA of slice k, so
+    // the call costs max(copy, PCIe) instead of their sum.
+    e = stage_h2d(d, hst, src, wbytes, st);
+  }
   uint64_t* hoff = reinterpret_cast<uint64_t*>(hst + meta_off);
   uint64_t* hlen = hoff + n;
   uint32_t* hini = reinterpret_cast<uint32_t*>(hlen + n);
@@ -895,14 +982,14 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     hlen[i] = lengths[i];
     hini[i] = init ? init[i] : init_all;
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(d + meta_off, hst + meta_off, total - meta_off, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dmeta, hst + meta_off, total - meta_off, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && as_region)
-    rc = do_region(s, d, wbytes, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
-                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, nullptr, nullptr,
+    rc = do_region(s, dwin, wbytes, reinterpret_cast<uint64_t*>(dmeta), reinterpret_cast<uint64_t*>(dmeta) + n,
+                   reinterpret_cast<uint32_t*>(dmeta + n * 16), 0, dout, n, flags, dws, ws, st, nullptr, nullptr,
                    /*checked=*/false);
   else if (e == hipSuccess)
-    rc = do_batch(s, d, reinterpret_cast<uint64_t*>(d + meta_off), reinterpret_cast<uint64_t*>(d + meta_off) + n,
-                  reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
+    rc = do_batch(s, dwin, reinterpret_cast<uint64_t*>(dmeta), reinterpret_cast<uint64_t*>(dmeta) + n,
+                  reinterpret_cast<uint32_t*>(dmeta + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
   else
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));

@@ -19,10 +19,14 @@
 // flags = 0 crossover (bytes checksummed per host-resident call), from
 // profiles/r05_shim_latency.jsonl: with the AVX-512 folding
 // host CRC the host wins at 32 MiB (0.84-1.08 vs 1.49-1.51 ms), the GPU at
-// 128 MiB (3.26-3.66 vs 5.29-5.70 ms); round 4's SSE4.2 host CRC crossed at
-// ~17 MiB.
+// 128 MiB (3.26-3.66 vs 5.29-5.70 ms) -> 64 MiB; with the SSE4.2 host CRC
+// (a CPU without VPCLMULQDQ, or NVL_CRC32C_HOST=sse) round 4 measured the
+// crossover at ~17 MiB -> 16 MiB (chosen by the host tier).
 #ifndef NVL_FRAMING_DEFAULT_GPU_MIN_BYTES
 #define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES (64ull << 20)
+#endif
+#ifndef NVL_FRAMING_DEFAULT_GPU_MIN_BYTES_SSE
+#define NVL_FRAMING_DEFAULT_GPU_MIN_BYTES_SSE (16ull << 20)
 #endif
 
 namespace nvl {
@@ -40,16 +44,20 @@ inline void store_le32(uint8_t* p, uint32_t v) {
 }
 
 // Host-resident batches smaller than this run on the calling thread's host
-// CRC when flags = 0 (the measured crossover).
-constexpr uint64_t kGpuMinBytes = NVL_FRAMING_DEFAULT_GPU_MIN_BYTES;
+// CRC when flags = 0 (the measured crossover of the host tier in use,
+// DESIGN.md §9).
+uint64_t default_gpu_min_bytes() {
+  return host_tier_id() >= 2 ? NVL_FRAMING_DEFAULT_GPU_MIN_BYTES : NVL_FRAMING_DEFAULT_GPU_MIN_BYTES_SSE;
+}
 
 uint64_t gpu_min_bytes() {
   static const uint64_t v = [] {
+    const uint64_t d = default_gpu_min_bytes();
     const char* e = getenv("NVL_FRAMING_GPU_MIN_BYTES");
-    if (!e || !*e) return kGpuMinBytes;
+    if (!e || !*e) return d;
     char* end = nullptr;
     const unsigned long long x = strtoull(e, &end, 0);
-    return (end && *end == '\0') ? (uint64_t)x : kGpuMinBytes;
+    return (end && *end == '\0') ? (uint64_t)x : d;
   }();
   return v;
 }

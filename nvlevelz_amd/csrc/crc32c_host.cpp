@@ -198,7 +198,7 @@ NVL_AVX512_TARGET uint32_t raw_vpclmul(uint32_t l, const uint8_t* p, size_t n) {
   const FoldTables& t = fold_tables();
   __m512i x0 = _mm512_loadu_si512(p), x1 = _mm512_loadu_si512(p + 64), x2 = _mm512_loadu_si512(p + 128),
           x3 = _mm512_loadu_si512(p + 192);
-  x0 = _mm512_xor_si512(x0, _mm512_castsi128_si512(_mm_cvtsi32_si128((int)l)));  // raw(l, w||r) = raw(0, (w^l)||r)
+  x0 = _mm512_xor_si512(x0, _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)l)));  // raw(l, w||r) = raw(0, (w^l)||r)
   p += 256;
   n -= 256;
   const __m512i k256 = kvec512(t.k256);
@@ -283,6 +283,8 @@ uint32_t host_extend(uint32_t init, const void* data, size_t n) {
 #endif
   return raw_slice8(l, p, n) ^ 0xffffffffu;
 }
+
+int host_tier_id() { return host_tier(); }
 
 const char* host_impl_name() {
   static const char* const kNames[] = {"slice-by-8", "sse4.2 crc32q x3", "avx512 vpclmulqdq fold + sse4.2"};

@@ -157,5 +157,7 @@ hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in,
 // CPU single-buffer Extend (crc32c_host.cpp) and the tier it chose.
 uint32_t host_extend(uint32_t init, const void* data, size_t n);
 const char* host_impl_name();
+// The host tier host_extend runs: 0 slice-by-8, 1 SSE4.2 crc32q, 2 AVX-512 folding.
+int host_tier_id();
 
 }  // namespace nvl

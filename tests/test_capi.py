@@ -165,3 +165,20 @@ def test_routed_workspace_is_bounded(L):
     big = L.lib.nvl_crc32c_batch_workspace_bytes(10_000_000)
     assert big < 700_000_000
     assert big - 32 * 10_000_000 >= 4 * (1 << 24)
+
+
+def test_workspace_sizes_stay_bounded():
+    """the checked entries reserve the routed call's region part
+    (32 B of event records per buffer + 4 B per chunk of the span, at most
+    2^24 chunks).  The sizes INTEGRATION.md §6 tabulates stay within these
+    bounds (no GPU: the library sizes for 256 CUs)."""
+    from nvlevelz_amd import _lib
+    L = _lib.lib
+    assert L.nvl_crc32c_batch_workspace_bytes(1) < 1 << 20
+    for n in (10**3, 10**5, 10**6, 10**7):
+        b = L.nvl_crc32c_batch_workspace_bytes(n)
+        r = L.nvl_crc32c_region_workspace_bytes(4096 * n, n)
+        assert b <= 60 * n + (64 << 20) + (1 << 20), (n, b)   # <= 60 B per buffer + the 64 MiB raw cap
+        assert r <= 56 * n + (1 << 20), (n, r)                # 32 B records + 4 B raw + the batch part
+    assert L.nvl_crc32c_batch_workspace_bytes(10**5) < 24 << 20
+    assert L.nvl_crc32c_fixed_workspace_bytes(4096, 4096, 10**7) == 0

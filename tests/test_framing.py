@@ -336,6 +336,22 @@ def test_sstable_trailers_golden(L):
         assert int.from_bytes(img[-4:], "little") == int(b["masked"])
 
 
+def test_engine_policy_follows_host_tier():
+    """the default crossover follows the host CRC tier -- 64 MiB
+    over the AVX-512 folding tier, 16 MiB over SSE4.2 (its measured ~17 MiB
+    crossover) and slice-by-8."""
+    code = ("import sys; sys.path.insert(0, %r); from nvlevelz_amd import _lib; "
+            "print(_lib.lib.nvl_crc32c_host_impl().decode(), _lib.lib.nvl_framing_gpu_min_bytes())" % ROOT)
+    env = {k: v for k, v in os.environ.items() if k not in ("NVL_FRAMING_GPU_MIN_BYTES", "NVL_CRC32C_HOST")}
+    for cap in ("sse", "table", None):
+        e = dict(env, NVL_CRC32C_HOST=cap) if cap else env
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, env=e)
+        assert r.returncode == 0, r.stderr
+        impl, m = r.stdout.rsplit(None, 1)
+        want = (64 << 20) if impl.startswith("avx512") else (16 << 20)
+        assert int(m) == want, (cap, impl, m)
+
+
 @pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
 def test_device_mode_fails_loudly_without_gpu(L):
     img = bytearray(b"abc" + bytes(5))

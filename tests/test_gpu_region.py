@@ -161,9 +161,11 @@ def test_region_unaligned_region_pointer(dev, C, port, skew):
 
 
 def test_region_other_layouts_are_correct(dev, C, port):
-    """Unsorted, overlapping and out-of-region batches take the serial path
-    (correct, slow); a sorted call on the same stream afterwards is fast and
-    correct again (the flag was re-zeroed)."""
+    """Unsorted, overlapping and out-of-region batches through the checked
+    entry: the plan sends them to the batch kernels, correct; a
+    sorted call on the same stream afterwards takes the region path and is
+    correct again.  (The region kernel's own per-buffer fallback for such
+    batches is test_region_shaped_flag_on_other_layouts.)"""
     rng = np.random.default_rng(5)
     host = port.fill(0x515, 0, 200_000)
     buf = torch.from_numpy(host).to(dev)
@@ -182,6 +184,56 @@ def test_region_other_layouts_are_correct(dev, C, port):
     got = _region(C, dev, region, offs_o, lens_o)
     assert np.array_equal(got, want)
     _check(C, dev, port, host, buf, offs_s, lens_s, 3)
+
+
+def test_region_shaped_flag_on_other_layouts(dev, C, port):
+    """NVL_CRC32C_FLAG_REGION_SHAPED on batches that are NOT region-shaped
+    (ADVICE r05): the one-launch region kernel runs them anyway, and the
+    header promises correct results -- buffers whose event records are
+    missing (unsorted, overlapping), lie outside the region, or are longer
+    than NVL_CRC32C_REGION_MAX_LEN (re-streamed halos) go through the
+    kernel's per-buffer fallback (fold_in's inside rule, the records'
+    buffer-index check).  Calls alternate with sorted ones on ONE caller
+    workspace, so every stale record of the previous call is present."""
+    rng = np.random.default_rng(77)
+    host = port.fill(0x5A9E, 0, 900_000)
+    buf = torch.from_numpy(host).to(dev)
+    region = buf[:600_000]
+    n = 400
+    wsb = max(C.region_workspace_bytes(900_000, 3 * n), C.region_workspace_bytes(600_000, 3 * n))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    lens_s = rng.integers(64, 1500, n)
+    offs_s, _ = _packed(port, lens_s, 3, 0, lead=11)
+
+    def run(r, offs, lens, name):
+        offs, lens = np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64)
+        inits = rng.integers(0, 2**32, size=len(offs), dtype=np.uint64).astype(np.uint32)
+        want = port.varlen(host, offs.astype(np.uint64), lens.astype(np.uint64), inits)
+        it = torch.from_numpy(inits.view(np.int32)).to(dev)
+        got = _u32(C.extend_region(r, _t64(offs, dev), _t64(lens, dev), it, workspace=ws, shaped=True))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (name, bad[:8], offs[bad[:8]], lens[bad[:8]])
+
+    lens_u = rng.integers(0, 6000, n)
+    offs_u = rng.integers(0, 600_000 - 6000, n)
+    run(region, offs_u, lens_u, "unsorted + overlapping")
+    run(region, offs_s, lens_s, "sorted after unsorted")
+    perm = rng.permutation(n)
+    run(region, offs_s[perm], lens_s[perm], "sorted blocks shuffled")
+    run(region, offs_s, lens_s, "sorted after shuffled")
+    ov = offs_s.copy()
+    ov[1::7] -= 40  # every 7th buffer starts inside its predecessor
+    run(region, ov, lens_s, "overlapping neighbours")
+    # buffers past the region's end (inside the allocation: caller memory)
+    offs_o = np.concatenate([offs_s[:50], [590_000, 599_990, 650_000]])
+    lens_o = np.concatenate([lens_s[:50], [20_000, 100, 5000]])
+    run(region, offs_o, lens_o, "outside the region")
+    # buffers over 128 KiB among short ones, sorted (halos spanning many
+    # workgroups' ranges, folded serially by their owner)
+    lens_l = np.array([100, 140_000, 3000, 300_000, 17, 131_073, 131_072, 4096], dtype=np.int64)
+    offs_l, _ = _packed(port, lens_l, 9, 0, lead=5)
+    run(buf, offs_l, lens_l, "buffers over NVL_CRC32C_REGION_MAX_LEN")
+    run(region, offs_s, lens_s, "sorted after long buffers")
 
 
 def test_region_many_small_and_windows(dev, C, port):

@@ -529,6 +529,7 @@ struct ThreadRes {
   DevSlab table_dev;      // nvl_sstable_verify_table_dev
   Staging table_pinned;
   hipEvent_t table_ev[kMaxDevices][2] = {};
+  hipEvent_t wait_ev[kMaxDevices] = {};  // blocking-sync events of wait_host_call
   bool registered = false;
 
   void enroll() {
@@ -547,6 +548,11 @@ struct ThreadRes {
         (void)hipSetDevice(d);
         (void)hipEventDestroy(e);
         e = nullptr;
+      }
+      if (wait_ev[d]) {
+        (void)hipSetDevice(d);
+        (void)hipEventDestroy(wait_ev[d]);
+        wait_ev[d] = nullptr;
       }
       if (!st[d]) continue;
       (void)hipSetDevice(d);
@@ -586,6 +592,23 @@ struct ThreadRes {
 thread_local ThreadRes t_res;
 
 hipStream_t thread_stream(int device) { return t_res.stream(device); }
+
+// The end of a synchronous host-resident call: wait for `st` (on `device`).
+// hipStreamSynchronize spins the calling core for the whole call, which is
+// the host CPU the GPU path is meant to give back (host
+// CPU-seconds per GiB); a call moving at least kBlockingWaitBytes sleeps on
+// a blocking-sync event instead (an interrupt wake-up costs tens of µs:
+// short calls keep the spin).
+constexpr uint64_t kBlockingWaitBytes = 4ull << 20;
+hipError_t wait_host_call(int device, hipStream_t st, uint64_t bytes) {
+  if (bytes >= kBlockingWaitBytes && device >= 0 && device < kMaxDevices) {
+    hipEvent_t& e = t_res.wait_ev[device];
+    if (!e && hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) e = nullptr;
+    if (e && hipEventRecord(e, st) == hipSuccess) return hipEventSynchronize(e);
+    (void)hipGetLastError();
+  }
+  return hipStreamSynchronize(st);
+}
 
 }  // namespace
 
@@ -815,7 +838,7 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
-  if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (wait_host_call(s->device, st, data_bytes) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
 }
 
@@ -994,7 +1017,7 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
-  if (hipStreamSynchronize(st) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (wait_host_call(s->device, st, wbytes) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
 }
 
@@ -1159,7 +1182,7 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
     if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out + i0, dout[k], m * 4, hipMemcpyDeviceToHost, st[k]));
   }
   for (int k = 0; k < 2; ++k)
-    if (hipStreamSynchronize(st[k]) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+    if (wait_host_call(s->device, st[k], n * stride) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
 }
 

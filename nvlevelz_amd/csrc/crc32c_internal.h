@@ -1,5 +1,6 @@
 // nvlevelz_amd/csrc/crc32c_internal.h -- internal interfaces between the
-// C-ABI layer (crc32c_capi.cpp) and the kernel launchers (crc32c_kernels.hip,
+// C-ABI layer (crc32c_capi.cpp) and the kernel launchers (crc32c_fixed.hip,
+// crc32c_batch.hip, crc32c_region.hip, crc32c_misc.hip,
 // crc32c_scan.hip).  Not installed; not part of the ABI.
 #pragma once
 #include <hip/hip_runtime_api.h>

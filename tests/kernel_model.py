@@ -1,6 +1,6 @@
 """Pure-Python model of the HIP engine's algorithm (test infrastructure).
 
-Mirrors nvlevelz_amd/csrc/crc32c_kernels.hip step for step -- end-aligned
+Mirrors nvlevelz_amd/csrc/crc32c_*.hip / crc32c_dev*.h step for step -- end-aligned
 4096-byte chunks, 64 lanes x 64-byte pieces, leading-zero masking and ~init
 injection, per-lane slice-by-4, the 6-level shift-operator butterfly, the
 per-wave contiguous chunk ranges with shift4096 accumulation, the per-wave
@@ -103,7 +103,7 @@ OVER = 0  # overhang (round-1 knob, removed from the kernels): a first chunk of 
 
 
 def chunks_of(L: int) -> int:
-    """Chunks of a buffer of L bytes (crc32c_kernels.hip chunks_for): END-aligned
+    """Chunks of a buffer of L bytes (crc32c_dev.h chunks_for): END-aligned
     4096-byte chunks (with an overhang, a first chunk of 4097..4096+OVER bytes
     is not split)."""
     return 1 if L <= CHUNK + OVER else (L - OVER + CHUNK - 1) // CHUNK
@@ -142,7 +142,7 @@ def group_fold(g, nlev: int):
 
 
 def head_class(hl: int) -> int:
-    """Lanes per head (crc32c_kernels.hip run_heads): 64-byte pieces, P = 1, 4, 16, 64."""
+    """Lanes per head (crc32c_dev_heads.h run_heads): 64-byte pieces, P = 1, 4, 16, 64."""
     return 1 if hl <= 64 else 4 if hl <= 256 else 16 if hl <= 1024 else 64
 
 
@@ -189,7 +189,7 @@ def head_raw(mem: bytes, p: int, L: int, J: int, s: int) -> int:
 
 
 def long_head(p: int, hl: int) -> bool:
-    """crc32c_kernels.hip run_heads: a head of 1025..4095 bytes runs as a whole
+    """crc32c_dev_heads.h run_heads: a head of 1025..4095 bytes runs as a whole
     chunk (long_heads) unless the buffer starts in the first 16 bytes of a
     4 KiB page."""
     return 1024 < hl < CHUNK and ((p >> 4) & 255) != 0
@@ -572,7 +572,7 @@ def quad_prefix(x: int, quad: bytes, o: int) -> int:
     return crc
 
 
-# ---- region path: the launch's partition (crc32c_kernels.hip run_region) ----
+# ---- region path: the launch's partition (crc32c_dev_region.h run_region) ----
 # Workgroup b of G owns the chunk range [B0, B1) = [nc b / G, nc (b+1) / G)
 # and the buffers [I_b, I_b+1), I_b = the first buffer ending after chunk
 # B0's start (I_0 = 0, I_G = n).  Its units: nfull two-chunk units, then
@@ -653,7 +653,7 @@ def region_span_stale(u: int, B0: int, nfull: int, nunits: int, nhalo: int, hc: 
     return B0 + h * U, (min(U, hc - h * U) if h < nhalo else 0)
 
 
-# ---- routed calls: the plan's verdict (crc32c_kernels.hip crc32c_route_plan,
+# ---- routed calls: the plan's verdict (crc32c_region.hip crc32c_route_plan,
 # route_region) ------------------------------------------------------------
 REGION_MAX_LEN = 128 << 10
 

@@ -15,20 +15,29 @@ from conftest import ROOT
 
 HIPCC = "/opt/rocm/bin/hipcc"
 CSRC = os.path.join(ROOT, "nvlevelz_amd", "csrc")
+# the kernel TUs (crc32c_kernels.hip until round 5)
+KERNEL_TUS = ["crc32c_fixed.hip", "crc32c_batch.hip", "crc32c_region.hip", "crc32c_misc.hip"]
 
 
 @pytest.fixture(scope="module")
 def usage(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    out = tmp_path_factory.mktemp("ru") / "k.o"
-    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "--offload-arch=gfx950",
-                        "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-c",
-                        os.path.join(CSRC, "crc32c_kernels.hip"), "-o", str(out),
-                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    kernels, cur = {}, None
-    for line in r.stderr.splitlines():
+    kernels = {}
+    for tu in KERNEL_TUS:
+        out = tmp_path_factory.mktemp("ru") / (tu + ".o")
+        r = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "--offload-arch=gfx950",
+                            "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-c",
+                            os.path.join(CSRC, tu), "-o", str(out),
+                            "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        _parse(r.stderr, kernels)
+    return kernels
+
+
+def _parse(stderr, kernels):
+    cur = None
+    for line in stderr.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
             cur = m.group(1)
@@ -66,7 +75,7 @@ def test_no_vgpr_spills(usage, name):
 
 def test_region_fold_claim_placement(usage):
     """The region fold deals its slices by SIMD (slice k to the waves on SIMD
-    k mod 4, crc32c_kernels.hip run_region).  Correctness does not depend on
+    k mod 4, crc32c_dev_region.h run_region).  Correctness does not depend on
     where the 16 waves land: a SIMD that holds none of them has its slices
     adopted by the lowest populated SIMD's waves.  The balance
     does: above 102 VGPRs (512 per lane and SIMD, granule 8) a SIMD takes at

@@ -5,7 +5,7 @@
    with bit 31 set is sign-extended into the high half.  That corrupted
    head-kernel item pointers and faulted a GPU in round 2 (DESIGN §3.4
    "Division").  Every call must go through the four helpers of
-   crc32c_kernels.hip (uniform_u32 / uniform_u64 / lane_u32 / lane_u64),
+   crc32c_dev.h (uniform_u32 / uniform_u64 / lane_u32 / lane_u64),
    whose 32-bit forms static_assert on wider operands and whose 64-bit forms
    move two uint32_t halves.
 2. No ablation or diagnostic variants in the product translation units:
@@ -61,7 +61,7 @@ def test_lane_reads_only_inside_the_helpers():
 
 
 def test_helpers_refuse_64bit_operands():
-    text = open(os.path.join(CSRC, "crc32c_kernels.hip")).read()
+    text = open(os.path.join(CSRC, "crc32c_dev.h")).read()
     for name in ("uniform_u32", "lane_u32"):
         body = [text[a:b] for a, b in _function_spans(text, (name,))]
         assert body and "static_assert(sizeof(T) <= 4" in body[0], name

@@ -236,7 +236,7 @@ def test_region_quad_prefix_from_checkpoints(port):
 
 
 def _grid_for(nc: int, num_cu: int = 256) -> int:
-    return max(1, min(num_cu, -(-nc // 16)))  # crc32c_kernels.hip grid_for
+    return max(1, min(num_cu, -(-nc // 16)))  # crc32c_launch.h grid_for
 
 
 @pytest.mark.parametrize("G", [None, 1, 4, 16, 256])

@@ -1,4 +1,4 @@
-"""The routed calls' layout rule (crc32c_kernels.hip crc32c_route_plan,
+"""The routed calls' layout rule (crc32c_region.hip crc32c_route_plan,
 modelled by tests/kernel_model.py route_plan_bad): what batch_dev accepts for
 the region path must never make the region path read a 4 KiB page that holds
 no buffer byte -- the only pages known to be mapped (buffers from different

@@ -1,5 +1,5 @@
 """Per-wave timeline of scheduler C (run_bufs) on a variable-length batch
-(diagnostic variant build: make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h"): start, after the LDS fill, end and
+(diagnostic variant build: make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS_crc32c_batch="-include ../../tools/diag/stamps.h"): start, after the LDS fill, end and
 chunks walked per wave.  CFG=v (10^5 x 4097 B, unfused plan) or CFG=3 (config 3,
 fused kernel)."""
 import ctypes, json, os, sys

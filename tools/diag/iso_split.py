@@ -1,7 +1,7 @@
 """Split one isolated config-2 launch: the stamps variant
 build (tools/diag/stamps.h: per wave s_memrealtime at start, after the LDS
 fill, at the end; 100 MHz) against the HIP events around the launch.
-    make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h"
+    make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS_crc32c_fixed="-include ../../tools/diag/stamps.h"
     LIB=build/libnvl_crc32c_stamps.so python tools/diag/iso_split.py [ITERS=30]
 Per launch: event_us (ordinary events before/after, idle queue), span_us (first
 wave start -> last wave end), outside = event - span (dispatch, completion and

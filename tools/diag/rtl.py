@@ -1,6 +1,6 @@
 """Phase timeline of the region kernel (run_region) from a diagnostic variant
 build with tools/diag/stamps.h force-included:
-    make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h"
+    make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS_crc32c_region="-include ../../tools/diag/stamps.h"
     CFG=v|r|3 LIB=build/libnvl_crc32c_stamps.so python tools/diag/rtl.py
 Stamps per wave (s_memrealtime, 100 MHz): 0 entry, 1 after the LDS fill
 barrier, 2 out of units, 3 after the fold barrier, 4 a slice's records in,

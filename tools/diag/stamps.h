@@ -1,7 +1,8 @@
 // tools/diag/stamps.h -- per-wave timeline instrumentation for a DIAGNOSTIC
-// variant build of nvlevelz_amd/csrc/crc32c_kernels.hip (never the shipped
-// library).  Force-included ahead of the kernel source:
-//   make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h"
+// variant build of ONE kernel TU (never the shipped library).  Force-included
+// ahead of that TU's source (its readers are defined once per library):
+//   make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS_crc32c_fixed="-include ../../tools/diag/stamps.h"
+// (crc32c_region for run_region's timelines, crc32c_batch for the body kernels)
 // It defines the hook macros the kernel source leaves as no-ops: per wave
 // {start, after the LDS table fill, end} s_memrealtime stamps (100 MHz) and
 // {XCC id, units processed}, read back by tools/diag/stamps.py through

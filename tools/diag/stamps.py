@@ -1,4 +1,4 @@
-"""Per-wave timeline of one fast-path launch (diagnostic variant build: make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h")."""
+"""Per-wave timeline of one fast-path launch (diagnostic variant build: make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS_crc32c_fixed="-include ../../tools/diag/stamps.h")."""
 import ctypes, os, sys
 import numpy as np, torch
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.getcwd()))

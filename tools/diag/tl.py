@@ -1,6 +1,6 @@
 """Phase timeline of the head kernel (run_heads) on a variable-length batch,
 from a diagnostic variant build with tools/diag/stamps.h force-included:
-    make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS="-include ../../tools/diag/stamps.h"
+    make -C nvlevelz_amd/csrc variant NAME=stamps VFLAGS_crc32c_region="-include ../../tools/diag/stamps.h"
     CFG=r|v|3|u LIB=build/libnvl_crc32c_stamps.so python tools/diag/tl.py
 (r, v, 3 are region-shaped and batch_dev now routes them to the region path;
 u -- shuffled aligned 4 KiB -- keeps the head kernel's work, in the route kernel)

@@ -197,6 +197,44 @@ NVL_API int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len,
  * per buffer for the region path, plus the batch path's workspace). */
 NVL_API size_t nvl_crc32c_region_workspace_bytes(uint64_t region_len, uint64_t n);
 
+/* ---- several devices, device-resident, one process ---------------------- */
+/* BASELINE config 5's form inside ONE process (a LevelDB process is one
+ * process: db/db_impl.cc:920-923 runs compactions on its own threads): the
+ * blocks already live on several GPUs, shard k in devices[k]'s HBM, and each
+ * shard is checksummed where it lies -- no block ever crosses xGMI.  Shard k
+ * is a fixed-stride batch (as nvl_crc32c_fixed_dev) with its results in
+ * `out` on the same device; `stream` is a stream of that device (NULL: its
+ * null stream).  Every shard is
+ * enqueued before the call returns (asynchronous, like nvl_crc32c_fixed_dev:
+ * synchronise each shard's stream); the calling thread's current device is
+ * left as it was.  A device may hold several shards. */
+typedef struct nvl_crc32c_shard {
+  int device;         /* HIP device holding base and out */
+  const void* base;   /* shard buffer i at base + i * stride, len bytes */
+  uint64_t stride;
+  uint64_t len;
+  uint64_t n;         /* buffers in the shard */
+  uint32_t* out;      /* n u32 results, on `device` */
+  void* stream;       /* hipStream_t of `device`, or NULL (its null stream) */
+} nvl_crc32c_shard;
+NVL_API int nvl_crc32c_fixed_dev_multi(const nvl_crc32c_shard* shards, int nshards, uint32_t init_all,
+                                       uint32_t flags);
+
+/* The shards' results gathered into ONE device array `dst` (on dst_device,
+ * ordered on `stream`, a stream of dst_device or NULL for its null stream):
+ * every shard's `out` is copied over xGMI (hipMemcpyPeerAsync,
+ * 4 bytes per block: the only cross-device traffic) after that shard's
+ * stream, then laid out by `layout`:
+ *   NVL_CRC32C_GATHER_CONCAT       shard 0's results, then shard 1's, ...
+ *   NVL_CRC32C_GATHER_ROUND_ROBIN  global block i from shard i mod nshards
+ *                                  (shard k must hold ceil((N - k) / nshards)
+ *                                  blocks of the N in total: config 5's split)
+ * Asynchronous on `stream`. */
+#define NVL_CRC32C_GATHER_CONCAT 0u
+#define NVL_CRC32C_GATHER_ROUND_ROBIN 1u
+NVL_API int nvl_crc32c_gather_dev(uint32_t* dst, int dst_device, const nvl_crc32c_shard* shards, int nshards,
+                                  uint32_t layout, void* stream);
+
 /* ---- batched, host-resident (end-to-end path) ---------------------------- */
 
 /* Host buffers in, host results out, synchronous: stages the buffers through

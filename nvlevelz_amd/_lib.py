@@ -65,6 +65,8 @@ SIGNATURES = {
                                            _vp]),
     "nvl_crc32c_region_workspace_bytes": (_sz, [_u64, _u64]),
     "nvl_crc32c_host_register": (_int, [_vp, _sz]),
+    "nvl_crc32c_fixed_dev_multi": (_int, [_vp, _int, _u32, _u32]),
+    "nvl_crc32c_gather_dev": (_int, [_vp, _int, _vp, _int, _u32, _vp]),
     "nvl_crc32c_host_unregister": (_int, [_vp]),
     "nvl_crc32c_host_registered": (_int, [_vp, _sz]),
     # include/nvl_framing.h
@@ -86,6 +88,15 @@ BLOCK_BAD_HANDLE = 4
 (TABLE_OK, TABLE_TOO_SHORT, TABLE_BAD_MAGIC, TABLE_BAD_FOOTER, TABLE_INDEX_UNREADABLE, TABLE_BAD_INDEX_BLOCK,
  TABLE_BAD_INDEX_ENTRY, TABLE_COMPRESSED_INDEX) = range(8)
 TBLOCK_INDEX, TBLOCK_METAINDEX, TBLOCK_META, TBLOCK_DATA = 0, 1, 2, 3
+
+
+GATHER_CONCAT, GATHER_ROUND_ROBIN = 0, 1
+
+
+class Shard(ctypes.Structure):
+    """nvl_crc32c_shard (include/nvl_crc32c.h)."""
+    _fields_ = [("device", _int), ("base", _vp), ("stride", _u64), ("len", _u64), ("n", _u64), ("out", _vp),
+                ("stream", _vp)]
 
 
 class TableBlock(ctypes.Structure):

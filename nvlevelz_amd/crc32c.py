@@ -390,6 +390,47 @@ def extend_region_host(region: np.ndarray, offsets, lengths, init=0, *, mask: bo
     return out
 
 
+def extend_fixed_multi(shards, init: int = 0, *, mask: bool = False):
+    """nvl_crc32c_fixed_dev_multi: one fixed-stride batch per device tensor,
+    every shard checksummed on the device holding it (one process, no bytes
+    cross devices).  shards: [(buf, stride, length, n)], buf a uint8 device
+    tensor (its device and current stream are the shard's).  Returns one
+    int32 result tensor per shard, on its device; asynchronous like
+    extend_fixed (synchronise the shards' streams before reading)."""
+    torch = _torch()
+    arr = (_lib.Shard * max(len(shards), 1))()
+    outs = []
+    for k, (buf, stride, length, n) in enumerate(shards):
+        _require_dev(buf, "buf", (torch.uint8, torch.int8))
+        if n and (n - 1) * stride + length > buf.numel():
+            raise ValueError(f"shard {k} extends past the end of its buffer")
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=buf.device)[:n]
+        outs.append(out)
+        arr[k] = _lib.Shard(buf.device.index, buf.data_ptr(), stride, length, n, out.data_ptr(), _stream_handle(buf))
+    rc = lib.nvl_crc32c_fixed_dev_multi(arr, len(shards), init & 0xFFFFFFFF, FLAG_MASK if mask else 0)
+    check(rc, "nvl_crc32c_fixed_dev_multi")
+    return outs
+
+
+def gather_dev(outs, device: int, *, round_robin: bool = False):
+    """nvl_crc32c_gather_dev: the shards' result tensors (extend_fixed_multi's)
+    gathered into one int32 tensor on `device` -- concatenated, or with
+    round_robin=True in config 5's global order (block i from shard i mod G).
+    Peer copies of 4 bytes per block; ordered after each shard's stream."""
+    torch = _torch()
+    arr = (_lib.Shard * max(len(outs), 1))()
+    N = 0
+    for k, o in enumerate(outs):
+        arr[k] = _lib.Shard(o.device.index, None, 0, 0, o.numel(), o.data_ptr(), _stream_handle(o))
+        N += o.numel()
+    dst = torch.empty(max(N, 1), dtype=torch.int32, device=torch.device("cuda", device))[:N]
+    rc = lib.nvl_crc32c_gather_dev(dst.data_ptr(), device, arr, len(outs),
+                                   _lib.GATHER_ROUND_ROBIN if round_robin else _lib.GATHER_CONCAT,
+                                   _stream_handle(dst))
+    check(rc, "nvl_crc32c_gather_dev")
+    return dst
+
+
 def multi_plan(offsets, lengths, ndev: int, min_bytes: int = 0) -> np.ndarray:
     """nvl_crc32c_multi_plan: the first buffer of each part (+ n at the end)."""
     o = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -420,5 +461,5 @@ def to_u32(t) -> np.ndarray:
 
 __all__ = ["extend", "value", "mask", "unmask", "kMaskDelta", "init", "gpu_accelerated",
            "extend_fixed", "FixedBatch", "extend_batch", "extend_region", "extend_batch_host", "extend_fixed_host",
-           "extend_region_host", "host_register", "host_unregister", "host_registered", "multi_plan", "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix",
+           "extend_region_host", "host_register", "host_unregister", "host_registered", "extend_fixed_multi", "gather_dev", "multi_plan", "fixed_workspace_bytes", "batch_workspace_bytes", "fill_splitmix",
            "to_u32", "Crc32cError"]

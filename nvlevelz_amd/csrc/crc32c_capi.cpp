@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -529,7 +530,7 @@ struct ThreadRes {
   DevSlab table_dev;      // nvl_sstable_verify_table_dev
   Staging table_pinned;
   hipEvent_t table_ev[kMaxDevices][2] = {};
-  hipEvent_t wait_ev[kMaxDevices] = {};  // blocking-sync events of wait_host_call
+  hipEvent_t wait_ev[kMaxDevices] = {};  // wait_host_call's events
   bool registered = false;
 
   void enroll() {
@@ -594,17 +595,31 @@ thread_local ThreadRes t_res;
 hipStream_t thread_stream(int device) { return t_res.stream(device); }
 
 // The end of a synchronous host-resident call: wait for `st` (on `device`).
-// hipStreamSynchronize spins the calling core for the whole call, which is
-// the host CPU the GPU path is meant to give back (host
-// CPU-seconds per GiB); a call moving at least kBlockingWaitBytes sleeps on
-// a blocking-sync event instead (an interrupt wake-up costs tens of µs:
-// short calls keep the spin).
+// hipStreamSynchronize (and, on this runtime, hipEventSynchronize of a
+// blocking-sync event too: measured, profiles/r06_host_register.jsonl) spins
+// the calling core for the whole call -- the host CPU the GPU path is meant
+// to give back (host CPU-seconds per GiB).  A call moving
+// at least kBlockingWaitBytes sleeps instead: until `t0` (the call's start)
+// + the least time its bytes need on the link (bytes / kSleepBytesPerSec;
+// PCIe Gen5 x16 moves ~53 GB/s here, so this never oversleeps the transfer),
+// then polls the stream's event every kPollUs.  Short calls keep the spin (their latency is
+// the shims' per-call cost).
 constexpr uint64_t kBlockingWaitBytes = 4ull << 20;
-hipError_t wait_host_call(int device, hipStream_t st, uint64_t bytes) {
+constexpr double kSleepBytesPerSec = 64e9;
+constexpr int kPollUs = 20;
+using Clock = std::chrono::steady_clock;
+hipError_t wait_host_call(int device, hipStream_t st, uint64_t bytes, Clock::time_point t0) {
   if (bytes >= kBlockingWaitBytes && device >= 0 && device < kMaxDevices) {
     hipEvent_t& e = t_res.wait_ev[device];
-    if (!e && hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) e = nullptr;
-    if (e && hipEventRecord(e, st) == hipSuccess) return hipEventSynchronize(e);
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    if (e && hipEventRecord(e, st) == hipSuccess) {
+      std::this_thread::sleep_until(t0 + std::chrono::microseconds((int64_t)((double)bytes / kSleepBytesPerSec * 1e6)));
+      for (;;) {
+        const hipError_t q = hipEventQuery(e);
+        if (q != hipErrorNotReady) return q;
+        std::this_thread::sleep_for(std::chrono::microseconds(kPollUs));
+      }
+    }
     (void)hipGetLastError();
   }
   return hipStreamSynchronize(st);
@@ -795,6 +810,7 @@ int nvl_crc32c_region_dev_timed(const void* region, uint64_t region_len, const u
 
 int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, const uint32_t* init,
                           uint32_t init_all, uint32_t* out, uint64_t n, uint32_t flags) {
+  const auto t_call = Clock::now();
   if (n == 0) return NVL_CRC32C_OK;
   if (!ptrs || !lengths || !out) return NVL_CRC32C_EINVAL;
   int rc = NVL_CRC32C_OK;
@@ -838,7 +854,7 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
-  if (wait_host_call(s->device, st, data_bytes) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (wait_host_call(s->device, st, data_bytes, t_call) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
 }
 
@@ -933,6 +949,7 @@ int nvl_crc32c_host_registered(const void* ptr, size_t bytes) {
 int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const uint64_t* offsets,
                                  const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out,
                                  uint64_t n, uint32_t flags) {
+  const auto t_call = Clock::now();
   if (n == 0) return NVL_CRC32C_OK;
   if (!offsets || !lengths || !out || (!region && region_len)) return NVL_CRC32C_EINVAL;
   if (flags & ~(NVL_CRC32C_FLAG_MASK | NVL_CRC32C_FLAG_HOST_ZERO_COPY)) return NVL_CRC32C_EINVAL;
@@ -1017,7 +1034,7 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
     rc = NVL_CRC32C_EHIP;
   if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
-  if (wait_host_call(s->device, st, wbytes) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (wait_host_call(s->device, st, wbytes, t_call) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
 }
 
@@ -1142,8 +1159,119 @@ int nvl_crc32c_batch_region_host_multi(const void* region, uint64_t region_len, 
   return NVL_CRC32C_OK;
 }
 
+// ---- several devices, device-resident ---------------------------------------
+
+// The stream a shard runs on (NULL: its device's null stream), checked to
+// belong to the shard's device.
+static int shard_stream(const nvl_crc32c_shard& sh, hipStream_t* st) {
+  *st = static_cast<hipStream_t>(sh.stream);
+  if (*st) {
+    int d = -1;
+    if (stream_device(*st, &d) != NVL_CRC32C_OK || d != sh.device) return NVL_CRC32C_EINVAL;
+  }
+  return NVL_CRC32C_OK;
+}
+
+int nvl_crc32c_fixed_dev_multi(const nvl_crc32c_shard* shards, int nshards, uint32_t init_all, uint32_t flags) {
+  if (!shards || nshards <= 0 || nshards > 4096) return NVL_CRC32C_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    (void)hipGetLastError();
+    ndev = 0;
+  }
+  for (int k = 0; k < nshards; ++k) {  // every argument first: nothing is enqueued for a bad call
+    const nvl_crc32c_shard& sh = shards[k];
+    if (sh.device < 0 || sh.n > (1ull << 40)) return NVL_CRC32C_EINVAL;
+    if (sh.n && (!sh.out || (!sh.base && sh.len))) return NVL_CRC32C_EINVAL;
+    if (sh.device >= ndev) return NVL_CRC32C_ENODEV;
+  }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  int rc = NVL_CRC32C_OK;
+  for (int k = 0; k < nshards && rc == NVL_CRC32C_OK; ++k) {
+    const nvl_crc32c_shard& sh = shards[k];
+    if (sh.n == 0) continue;
+    DeviceState* s = state_for(sh.device, &rc);
+    if (!s) break;
+    hipStream_t st = nullptr;
+    if ((rc = shard_stream(sh, &st)) != NVL_CRC32C_OK) break;
+    if (hipSetDevice(sh.device) != hipSuccess) {
+      rc = NVL_CRC32C_ENODEV;
+      break;
+    }
+    rc = do_fixed(s, sh.base, sh.stride, sh.len, sh.n, nullptr, init_all, sh.out, flags, nullptr, 0, st);
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return rc;
+}
+
+int nvl_crc32c_gather_dev(uint32_t* dst, int dst_device, const nvl_crc32c_shard* shards, int nshards,
+                          uint32_t layout, void* stream) {
+  if (!dst || !shards || nshards <= 0 || nshards > 4096 || layout > NVL_CRC32C_GATHER_ROUND_ROBIN)
+    return NVL_CRC32C_EINVAL;
+  uint64_t N = 0;
+  for (int k = 0; k < nshards; ++k) {
+    if (shards[k].n && !shards[k].out) return NVL_CRC32C_EINVAL;
+    N += shards[k].n;
+  }
+  if (layout == NVL_CRC32C_GATHER_ROUND_ROBIN)
+    for (int k = 0; k < nshards; ++k)
+      if (shards[k].n != (N > (uint64_t)k ? (N - (uint64_t)k + nshards - 1) / (uint64_t)nshards : 0))
+        return NVL_CRC32C_EINVAL;
+  int rc = NVL_CRC32C_OK;
+  if (!state_for(dst_device, &rc)) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);  // (NULL: dst_device's null stream)
+  if (st) {
+    int d = -1;
+    if (stream_device(st, &d) != NVL_CRC32C_OK || d != dst_device) return NVL_CRC32C_EINVAL;
+  }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(dst_device) != hipSuccess) return NVL_CRC32C_ENODEV;
+  uint32_t* tmp = nullptr;
+  const bool rr = layout == NVL_CRC32C_GATHER_ROUND_ROBIN && nshards > 1;
+  hipError_t e = rr ? hipMallocAsync(reinterpret_cast<void**>(&tmp), std::max<uint64_t>(N, 1) * 4, st) : hipSuccess;
+  uint32_t* to = rr ? tmp : dst;
+  uint64_t pos = 0;
+  for (int k = 0; k < nshards && e == hipSuccess; ++k) {
+    const nvl_crc32c_shard& sh = shards[k];
+    if (sh.n) {
+      // after the shard's own stream (its results), then the copy: a peer
+      // copy over xGMI for another device, a device copy for the same one
+      hipStream_t ss = nullptr;
+      if (shard_stream(sh, &ss) != NVL_CRC32C_OK) {
+        e = hipErrorInvalidValue;
+        break;
+      }
+      if (ss != st || sh.device != dst_device) {
+        hipEvent_t ev = nullptr;
+        if ((e = hipSetDevice(sh.device)) == hipSuccess &&
+            (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) == hipSuccess &&
+            (e = hipEventRecord(ev, ss)) == hipSuccess && (e = hipSetDevice(dst_device)) == hipSuccess)
+          e = hipStreamWaitEvent(st, ev, 0);
+        if (ev) (void)hipEventDestroy(ev);  // (released once the recorded work is done)
+        (void)hipSetDevice(dst_device);
+      }
+      if (e == hipSuccess)
+        e = sh.device == dst_device
+                ? hipMemcpyAsync(to + pos, sh.out, sh.n * 4, hipMemcpyDeviceToDevice, st)
+                : hipMemcpyPeerAsync(to + pos, dst_device, sh.out, sh.device, sh.n * 4, st);
+    }
+    pos += sh.n;
+  }
+  if (e == hipSuccess && rr) e = launch_interleave_rr(tmp, N, (uint32_t)nshards, dst, st);
+  if (tmp) (void)hipFreeAsync(tmp, st);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return NVL_CRC32C_EHIP;
+  }
+  return NVL_CRC32C_OK;
+}
+
 int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint64_t n, const uint32_t* init,
                           uint32_t init_all, uint32_t* out, uint32_t flags) {
+  const auto t_call = Clock::now();
   if (n == 0) return NVL_CRC32C_OK;
   if (!base || !out) return NVL_CRC32C_EINVAL;
   int rc = NVL_CRC32C_OK;
@@ -1182,7 +1310,7 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
     if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out + i0, dout[k], m * 4, hipMemcpyDeviceToHost, st[k]));
   }
   for (int k = 0; k < 2; ++k)
-    if (wait_host_call(s->device, st[k], n * stride) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+    if (wait_host_call(s->device, st[k], n * stride, t_call) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
   return rc;
 }
 

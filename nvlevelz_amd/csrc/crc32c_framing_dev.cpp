@@ -210,10 +210,7 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   //    blocks + meta blocks + index pieces.  A zero-length filler sits at the
   //    index block's offset (between the meta blocks and the first piece, so
   //    the slots stay in file order); a meta slot that is not read gets length
-  //    0 at the previous slot's end for the same reason.  (A table whose
-  //    blocks are out of file order still verifies: nvl_crc32c_region_dev's
-  //    plan finds the batch not region-shaped and runs it on the batch
-  //    kernels)
+  //    0 at the previous slot's end for the same reason.
   const uint64_t nf = nm_max;
   uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
   uint8_t* mv = pin + p_slots + nf * 16;
@@ -244,7 +241,16 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
              hipMemcpyAsync(blen + nr, ms + nf, nf * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
              hipMemcpyAsync(vk + nr, mv, nf, hipMemcpyHostToDevice, st) != hipSuccess))
     return NVL_CRC32C_EHIP;
-  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, n, 0, ws, wsb, st);
+  // One launch (NVL_CRC32C_FLAG_REGION_SHAPED): a table's slots are in file
+  // order by construction (table/table_builder.cc writes data blocks, meta
+  // blocks, the metaindex and the index in sequence, and the index lists the
+  // data blocks in key = file order), so the routed call's plan and body
+  // launches (~8 µs per call) would only confirm it.  A
+  // corrupt or crafted index whose handles are out of order or overlap still
+  // gets every CRC right: the region kernel checksums a buffer it has no
+  // event records for on its per-buffer path (slower; tests/test_table_verify.py
+  // ::test_table_dev_out_of_order_index).
+  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, n, NVL_CRC32C_FLAG_REGION_SHAPED, ws, wsb, st);
   if (rc != NVL_CRC32C_OK) return rc;
   const size_t res_bytes = kResHead + 4 * np + nm;
   uint8_t* res = pin + p_res;

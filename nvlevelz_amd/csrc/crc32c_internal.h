@@ -122,6 +122,8 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* ws);
 
+// dst[i] = shard (i mod G)'s result (i div G) from the shards' results concatenated (nvl_crc32c_gather_dev)
+hipError_t launch_interleave_rr(const uint32_t* src, uint64_t N, uint32_t G, uint32_t* dst, hipStream_t st);
 hipError_t launch_read_probe(const void* src, uint64_t bytes, uint32_t* sink, hipStream_t st);
 hipError_t launch_fill(void* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t first_block, uint64_t block_step,
                        uint64_t seed, hipStream_t st);

@@ -54,7 +54,26 @@ __global__ void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t words_
   }
 }
 
+// Round-robin interleave of gathered shard results (nvl_crc32c_gather_dev):
+// src holds shard 0's c_0 results, then shard 1's, ... (c_k = ceil((N-k)/G));
+// dst[i] = shard (i mod G)'s result (i div G).
+__global__ void interleave_rr_kernel(const uint32_t* __restrict__ src, uint64_t N, uint32_t G,
+                                     uint32_t* __restrict__ dst) {
+  const uint64_t q = N / G, r = N % G;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = i % G, j = i / G;
+    dst[i] = src[k * q + min<uint64_t>(k, r) + j];  // shard k starts after k shards of q (+1 for the first r)
+  }
+}
+
 }  // namespace dev
+
+hipError_t launch_interleave_rr(const uint32_t* src, uint64_t N, uint32_t G, uint32_t* dst, hipStream_t st) {
+  if (N == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((N + 255) / 256, 65536);
+  hipLaunchKernelGGL(dev::interleave_rr_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, src, N, G, dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_trailer_verdicts(const void* file, const uint64_t* off, const uint64_t* len1, const uint32_t* crc,
                                    uint64_t n, uint8_t* verdict, hipStream_t st) {

@@ -1,0 +1,122 @@
+"""Several devices, device-resident, one process (nvl_crc32c_fixed_dev_multi,
+nvl_crc32c_gather_dev; VERDICT r05 missing #3): every shard is checksummed on
+the device holding it, and the results are gathered into one device array,
+concatenated or in BASELINE config 5's round-robin order.
+
+The box has one GPU, so the shards are several buffers on device 0 (the
+entries take one shard per (device, buffer) and a device may hold several):
+the per-shard dispatch, the stream ordering and both gather layouts are what
+is checked; the peer (xGMI) copy path runs only on a multi-GPU node.
+CPU cases: argument checks, nothing enqueued for a bad call."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import gpu_present
+from nvlevelz_amd import _lib
+from nvlevelz_amd import crc32c as C
+
+L = _lib.lib
+
+
+def _shards(*sh):
+    arr = (_lib.Shard * max(len(sh), 1))()
+    for k, s in enumerate(sh):
+        arr[k] = s
+    return arr
+
+
+def test_multi_argument_checks():
+    out = (ctypes.c_uint32 * 4)()
+    base = (ctypes.c_uint8 * 4096)()
+    ok = _lib.Shard(0, ctypes.addressof(base), 4096, 4096, 1, ctypes.addressof(out), None)
+    assert L.nvl_crc32c_fixed_dev_multi(None, 1, 0, 0) == _lib.EINVAL
+    assert L.nvl_crc32c_fixed_dev_multi(_shards(ok), 0, 0, 0) == _lib.EINVAL
+    assert L.nvl_crc32c_fixed_dev_multi(_shards(_lib.Shard(-1, ctypes.addressof(base), 4096, 4096, 1,
+                                                           ctypes.addressof(out), None)), 1, 0, 0) == _lib.EINVAL
+    assert L.nvl_crc32c_fixed_dev_multi(_shards(_lib.Shard(0, None, 4096, 4096, 1, ctypes.addressof(out), None)),
+                                        1, 0, 0) == _lib.EINVAL
+    assert L.nvl_crc32c_fixed_dev_multi(_shards(_lib.Shard(0, ctypes.addressof(base), 4096, 4096, 1, None, None)),
+                                        1, 0, 0) == _lib.EINVAL
+    # gather: bad layout, a round-robin split that is not config 5's
+    assert L.nvl_crc32c_gather_dev(ctypes.addressof(out), 0, _shards(ok), 1, 7, None) == _lib.EINVAL
+    a = _lib.Shard(0, None, 0, 0, 1, ctypes.addressof(out), None)
+    b = _lib.Shard(0, None, 0, 0, 3, ctypes.addressof(out), None)
+    assert L.nvl_crc32c_gather_dev(ctypes.addressof(out), 0, _shards(a, b), 2, _lib.GATHER_ROUND_ROBIN,
+                                   None) == _lib.EINVAL
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-GPU behaviour")
+def test_multi_without_a_device():
+    out = (ctypes.c_uint32 * 4)()
+    base = (ctypes.c_uint8 * 4096)()
+    ok = _lib.Shard(0, ctypes.addressof(base), 4096, 4096, 1, ctypes.addressof(out), None)
+    assert L.nvl_crc32c_fixed_dev_multi(_shards(ok), 1, 0, 0) in (_lib.ENODEV, _lib.EHIP)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    C.init(0)
+    return torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
+def test_round_robin_shards_reassemble_config5_order(dev, port, G):
+    """N blocks of the config-5 stream split round-robin over G shards (shard
+    k = global blocks k, k + G, ...: fill_splitmix's block_step), checksummed
+    by fixed_dev_multi, gathered round-robin: the global CRC array equals the
+    oracle's over the first N blocks, and the concatenated gather equals the
+    shards in order."""
+    import torch
+    N, B = 5003, 4096
+    bufs, shards = [], []
+    for k in range(G):
+        nk = (N - k + G - 1) // G
+        b = torch.empty(max(nk, 1) * B, dtype=torch.uint8, device=dev)
+        C.fill_splitmix(b, nk, B, 0x5EED0005, first_block=k, block_step=G)
+        bufs.append(b)
+        shards.append((b, B, B, nk))
+    outs = C.extend_fixed_multi(shards)
+    rr = C.gather_dev(outs, 0, round_robin=True)
+    cat = C.gather_dev(outs, 0)
+    torch.cuda.synchronize()
+    whole = port.fixed(port.fill(0x5EED0005, 0, N * B), B, B, N)
+    assert np.array_equal(C.to_u32(rr), whole)
+    assert np.array_equal(C.to_u32(cat), np.concatenate([C.to_u32(o) for o in outs]))
+    for k, o in enumerate(outs):
+        assert np.array_equal(C.to_u32(o), whole[k::G]), k
+
+
+@pytest.mark.gpu
+def test_multi_shapes_mask_and_streams(dev, port):
+    """Shards of different shapes (aligned 4 KiB, odd stride and length,
+    multi-chunk), Mask, an empty shard, and shards on their own streams:
+    every result equals the oracle."""
+    import torch
+    host = port.fill(0x3131, 0, 3 << 20)
+    buf = torch.from_numpy(host).to(dev)
+    specs = [(0, 4096, 4096, 300), (7, 5001, 4999, 200), (4096 * 400, 16384, 12288, 60), (100, 4096, 4096, 0)]
+    streams = [torch.cuda.Stream(dev) for _ in specs]
+    shards = []
+    for (o, stride, ln, n), s in zip(specs, streams):
+        with torch.cuda.stream(s):
+            shards.append((buf[o:], stride, ln, n))
+    torch.cuda.synchronize()
+    outs = []
+    for sh, s in zip(shards, streams):  # each shard on its own stream (the stream current when it is passed)
+        with torch.cuda.stream(s):
+            outs += C.extend_fixed_multi([sh], mask=True)
+    torch.cuda.synchronize()
+    for (o, stride, ln, n), out in zip(specs, outs):
+        want = port.fixed(host[o:], stride, ln, n) if n else np.zeros(0, np.uint32)
+        assert np.array_equal(C.to_u32(out), np.array([port.mask(int(x)) for x in want], dtype=np.uint32))
+    outs2 = C.extend_fixed_multi(shards[:3])
+    cat = C.gather_dev(outs2, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(C.to_u32(cat), np.concatenate([port.fixed(host[o:], st, ln, n) for o, st, ln, n in specs[:3]]))

@@ -238,6 +238,48 @@ def test_table_dev_index_parse_at_size(L, port, interval, damage):
     assert data_bad == (nflip + 2 if damage else 0)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["shuffled", "overlapping"])
+def test_table_dev_out_of_order_index(L, port, mode):
+    """An index whose handles are NOT in file order (a crafted or corrupt
+    table: keys in order, handles permuted, or every 5th pointing back into
+    its predecessor): nvl_sstable_verify_table_dev runs its batch as ONE
+    region-kernel launch (NVL_CRC32C_FLAG_REGION_SHAPED, the slots of a
+    well-formed table are in file order), whose per-buffer path must still
+    give every block the host walk's verdict."""
+    if not gpu_present():
+        pytest.skip("no GPU")
+    import time
+    rng = np.random.default_rng(23)
+    w = tc._Writer(port)
+    pool = rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes()
+    hs = []
+    for b in range(4000):
+        n = int(rng.integers(1, 4000))
+        s = int(rng.integers(0, len(pool) - n))
+        hs.append(w.raw(pool[s:s + n], int(rng.integers(0, 2))))
+    if mode == "shuffled":
+        hs = [hs[i] for i in rng.permutation(len(hs))]
+    else:
+        hs = [(o - (min(200, o) if i % 5 == 4 else 0), n) for i, (o, n) in enumerate(hs)]
+    ents = [(b"user-key-%012d" % b, tc.handle(*h)) for b, h in enumerate(hs)]
+    filt = w.raw(pool[:777])
+    meta_h = w.raw(tc.block([(b"filter.leveldb.BuiltinBloomFilter2", tc.handle(*filt))], 16))
+    index_h = w.raw(tc.block(ents, 1))
+    foot = tc.handle(*meta_h) + tc.handle(*index_h)
+    w.img += foot + bytes(40 - len(foot)) + tc.MAGIC.to_bytes(8, "little")
+    img = bytes(w.img)
+    want = verify(L, img, HOST)
+    t0 = time.perf_counter()
+    got = verify_dev(L, img)
+    el = time.perf_counter() - t0
+    assert got == want, [(a, b) for a, b in zip(got[1], want[1]) if a != b][:5]
+    assert len(got[1]) == 4000 + 3
+    if mode == "overlapping":
+        assert sum(b[3] != 0 for b in want[1] if b[2] == 3) > 0  # the shifted handles fail their checks
+    assert el < 5.0, el
+
+
 def test_table_verify_dev_arguments(L):
     lib = L.lib
     n = ctypes.c_size_t(7)

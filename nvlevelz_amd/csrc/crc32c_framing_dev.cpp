@@ -241,16 +241,20 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
              hipMemcpyAsync(blen + nr, ms + nf, nf * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
              hipMemcpyAsync(vk + nr, mv, nf, hipMemcpyHostToDevice, st) != hipSuccess))
     return NVL_CRC32C_EHIP;
-  // One launch (NVL_CRC32C_FLAG_REGION_SHAPED): a table's slots are in file
-  // order by construction (table/table_builder.cc writes data blocks, meta
-  // blocks, the metaindex and the index in sequence, and the index lists the
-  // data blocks in key = file order), so the routed call's plan and body
-  // launches (~8 µs per call) would only confirm it.  A
-  // corrupt or crafted index whose handles are out of order or overlap still
-  // gets every CRC right: the region kernel checksums a buffer it has no
-  // event records for on its per-buffer path (slower; tests/test_table_verify.py
-  // ::test_table_dev_out_of_order_index).
-  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, n, NVL_CRC32C_FLAG_REGION_SHAPED, ws, wsb, st);
+  // Up to kShapedMaxSlots slots, one launch (NVL_CRC32C_FLAG_REGION_SHAPED):
+  // a table's slots are in file order by construction (table/table_builder.cc
+  // writes data blocks, meta blocks, the metaindex and the index in sequence,
+  // and the index lists the data blocks in key = file order), so the routed
+  // call's plan and body launches (~8 µs per call) would only
+  // confirm it.  A corrupt or crafted index whose handles are out of order or
+  // overlap still gets every CRC right from the region kernel's per-buffer
+  // path -- slowly: 10^4 shuffled 4 KiB blocks 6.9 ms, 10^5 62 ms
+  // (tools/shaped_fallback_time.py, profiles/r06_shaped_fallback.jsonl) --
+  // so larger tables keep the checked entry, whose plan sends such a batch to
+  // the batch kernels (tests/test_table_verify.py::test_table_dev_out_of_order_index).
+  constexpr uint64_t kShapedMaxSlots = 8192;
+  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, n,
+                                 n <= kShapedMaxSlots ? NVL_CRC32C_FLAG_REGION_SHAPED : 0u, ws, wsb, st);
   if (rc != NVL_CRC32C_OK) return rc;
   const size_t res_bytes = kResHead + 4 * np + nm;
   uint8_t* res = pin + p_res;

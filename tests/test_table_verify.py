@@ -239,14 +239,15 @@ def test_table_dev_index_parse_at_size(L, port, interval, damage):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["shuffled", "overlapping"])
-def test_table_dev_out_of_order_index(L, port, mode):
+@pytest.mark.parametrize("mode,nblocks", [("shuffled", 4000), ("overlapping", 4000), ("shuffled", 12000)])
+def test_table_dev_out_of_order_index(L, port, mode, nblocks):
     """An index whose handles are NOT in file order (a crafted or corrupt
     table: keys in order, handles permuted, or every 5th pointing back into
     its predecessor): nvl_sstable_verify_table_dev runs its batch as ONE
-    region-kernel launch (NVL_CRC32C_FLAG_REGION_SHAPED, the slots of a
-    well-formed table are in file order), whose per-buffer path must still
-    give every block the host walk's verdict."""
+    region-kernel launch up to 8192 slots (NVL_CRC32C_FLAG_REGION_SHAPED, the
+    slots of a well-formed table are in file order), whose per-buffer path
+    must still give every block the host walk's verdict; a larger table keeps
+    the checked entry (its plan sends the batch to the batch kernels)."""
     if not gpu_present():
         pytest.skip("no GPU")
     import time
@@ -254,7 +255,7 @@ def test_table_dev_out_of_order_index(L, port, mode):
     w = tc._Writer(port)
     pool = rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes()
     hs = []
-    for b in range(4000):
+    for b in range(nblocks):
         n = int(rng.integers(1, 4000))
         s = int(rng.integers(0, len(pool) - n))
         hs.append(w.raw(pool[s:s + n], int(rng.integers(0, 2))))
@@ -274,7 +275,7 @@ def test_table_dev_out_of_order_index(L, port, mode):
     got = verify_dev(L, img)
     el = time.perf_counter() - t0
     assert got == want, [(a, b) for a, b in zip(got[1], want[1]) if a != b][:5]
-    assert len(got[1]) == 4000 + 3
+    assert len(got[1]) == nblocks + 3
     if mode == "overlapping":
         assert sum(b[3] != 0 for b in want[1] if b[2] == 3) > 0  # the shifted handles fail their checks
     assert el < 5.0, el

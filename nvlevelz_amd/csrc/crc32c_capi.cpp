@@ -526,6 +526,7 @@ std::vector<ThreadRes*> g_tr;
 struct ThreadRes {
   hipStream_t st[kMaxDevices] = {};
   Staging staging;
+  Staging results;  // pinned landing area of the host entries' results (see wait_host_call)
   HostPipe pipe;
   DevSlab table_dev;      // nvl_sstable_verify_table_dev
   Staging table_pinned;
@@ -567,6 +568,7 @@ struct ThreadRes {
     if (table_dev.device >= 0) (void)hipSetDevice(table_dev.device);
     table_dev.release();
     staging.release();
+    results.release();
     table_pinned.release();
     if (prev >= 0) (void)hipSetDevice(prev);
   }
@@ -596,7 +598,7 @@ hipStream_t thread_stream(int device) { return t_res.stream(device); }
 
 // The end of a synchronous host-resident call: wait for `st` (on `device`).
 // hipStreamSynchronize (and, on this runtime, hipEventSynchronize of a
-// blocking-sync event too: measured, profiles/r06_host_register.jsonl) spins
+// blocking-sync event too: measured, profiles/r06/host_cpu_probe.jsonl) spins
 // the calling core for the whole call -- the host CPU the GPU path is meant
 // to give back (host CPU-seconds per GiB).  A call moving
 // at least kBlockingWaitBytes sleeps instead: until `t0` (the call's start)
@@ -608,6 +610,11 @@ constexpr uint64_t kBlockingWaitBytes = 4ull << 20;
 constexpr double kSleepBytesPerSec = 64e9;
 constexpr int kPollUs = 20;
 using Clock = std::chrono::steady_clock;
+// The results of a host entry land here (pinned): a D2H into the caller's
+// pageable `out` would have the runtime wait for the stream inside the copy
+// call -- spinning the calling core for the whole call (measured,
+// tools/host_cpu_probe.py: ~1 core per call, profiles/r06/host_cpu_probe.jsonl).
+uint32_t* pinned_results(uint64_t n) { return static_cast<uint32_t*>(t_res.results.get(std::max<uint64_t>(n, 1) * 4)); }
 hipError_t wait_host_call(int device, hipStream_t st, uint64_t bytes, Clock::time_point t0) {
   if (bytes >= kBlockingWaitBytes && device >= 0 && device < kMaxDevices) {
     hipEvent_t& e = t_res.wait_ev[device];
@@ -852,9 +859,12 @@ int nvl_crc32c_batch_host(const void* const* ptrs, const uint64_t* lengths, cons
                   reinterpret_cast<uint32_t*>(d + meta_off + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
   else
     rc = NVL_CRC32C_EHIP;
-  if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
+  uint32_t* hres = pinned_results(n);
+  if (!hres && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(hres, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
   if (wait_host_call(s->device, st, data_bytes, t_call) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) memcpy(out, hres, n * 4);
   return rc;
 }
 
@@ -1032,9 +1042,12 @@ int nvl_crc32c_batch_region_host(const void* region, uint64_t region_len, const 
                   reinterpret_cast<uint32_t*>(dmeta + n * 16), 0, dout, n, flags, dws, ws, st, max_len);
   else
     rc = NVL_CRC32C_EHIP;
-  if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out, dout, n * 4, hipMemcpyDeviceToHost, st));
+  uint32_t* hres = pinned_results(n);
+  if (!hres && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(hres, dout, n * 4, hipMemcpyDeviceToHost, st));
   (void)hipFreeAsync(d, st);
   if (wait_host_call(s->device, st, wbytes, t_call) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) memcpy(out, hres, n * 4);
   return rc;
 }
 
@@ -1299,6 +1312,8 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
     dws[k] = reinterpret_cast<uint8_t*>(dini[k] + per) + 256 - ((uintptr_t)(dini[k] + per) & 255);
   }
   const uint8_t* hb = static_cast<const uint8_t*>(base);
+  uint32_t* hres = pinned_results(n);
+  if (!hres) return NVL_CRC32C_EHIP;
   for (uint64_t i0 = 0, k = 0; rc == NVL_CRC32C_OK && i0 < n; i0 += per, k ^= 1) {
     const uint64_t m = std::min<uint64_t>(per, n - i0);
     const uint64_t bytes = (m - 1) * stride + len;
@@ -1307,10 +1322,11 @@ int nvl_crc32c_fixed_host(const void* base, uint64_t stride, uint64_t len, uint6
     if (e != hipSuccess) { rc = NVL_CRC32C_EHIP; break; }
     rc = do_fixed(s, dbuf[k], stride, len, m, init ? dini[k] : nullptr, init_all, dout[k], flags, dws[k], ws,
                   st[k]);
-    if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(out + i0, dout[k], m * 4, hipMemcpyDeviceToHost, st[k]));
+    if (rc == NVL_CRC32C_OK) rc = hip_rc(hipMemcpyAsync(hres + i0, dout[k], m * 4, hipMemcpyDeviceToHost, st[k]));
   }
   for (int k = 0; k < 2; ++k)
     if (wait_host_call(s->device, st[k], n * stride, t_call) != hipSuccess && rc == NVL_CRC32C_OK) rc = NVL_CRC32C_EHIP;
+  if (rc == NVL_CRC32C_OK) memcpy(out, hres, n * 4);
   return rc;
 }
 

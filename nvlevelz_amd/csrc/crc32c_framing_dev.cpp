@@ -249,7 +249,7 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   // confirm it.  A corrupt or crafted index whose handles are out of order or
   // overlap still gets every CRC right from the region kernel's per-buffer
   // path -- slowly: 10^4 shuffled 4 KiB blocks 6.9 ms, 10^5 62 ms
-  // (tools/shaped_fallback_time.py, profiles/r06_shaped_fallback.jsonl) --
+  // (tools/shaped_fallback_time.py, profiles/r06/shaped_fallback.jsonl) --
   // so larger tables keep the checked entry, whose plan sends such a batch to
   // the batch kernels (tests/test_table_verify.py::test_table_dev_out_of_order_index).
   constexpr uint64_t kShapedMaxSlots = 8192;

@@ -627,6 +627,17 @@ def main():
         pe[1].record(stream)
         torch.cuda.synchronize()
         probe = {"bytes": nb, "period_us": pe[0].elapsed_time(pe[1]) * 1e3 / args.probe}
+        # the same read-only kernel from an idle queue, as the isolated CRC
+        # launches above: what this box's memory system gives ONE launch after
+        # an idle gap (isolated calls vary 65-74 us from
+        # box to box -- the ratio names the kernel's share of it)
+        ip = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
+        for k in range(K):
+            ip[2 * k].record(stream)
+            lib.nvl_crc32c_read_probe(buf.data_ptr(), nb, sink.data_ptr(), stream.cuda_stream)
+            ip[2 * k + 1].record(stream)
+            torch.cuda.synchronize()
+        probe["isolated_median_us"] = float(np.median([ip[2 * k].elapsed_time(ip[2 * k + 1]) * 1e3 for k in range(K)]))
     # the slowest rank's own window (each rank's elapsed ends at its own
     # synchronize; the closing barrier is timed apart) and every rank's period
     rows = shard.gather_floats([elapsed, tw["period_s"], tw["barrier_after_s"], n_local], red_dev)
@@ -764,6 +775,14 @@ def main():
                         "roofline.achieved / this rate (the short timed window, which still ramps); "
                         "sustained_over_ceiling = the same for roofline.sustained's mean period, both ramped "
                         "(DESIGN.md section 4)" % args.probe}
+            line["roofline"]["read_ceiling"]["isolated_period_us"] = round(probe["isolated_median_us"], 2)
+            line["roofline"]["read_ceiling"]["isolated_kernel_over_ceiling"] = round(
+                probe["isolated_median_us"] / (float(np.median(iso_ms)) * 1e3), 4)
+            line["roofline"]["read_ceiling"]["isolated_what"] = (
+                "the read-only probe launched from an idle queue like isolated_median_us (event before and "
+                "after, synchronize between launches; median of K): isolated_kernel_over_ceiling = its "
+                "period / the CRC kernel's isolated median -- the share of an isolated call's time the memory "
+                "system's idle-to-busy ramp alone accounts for (DESIGN.md section 4)")
             if sus:
                 line["roofline"]["read_ceiling"]["sustained_over_ceiling"] = round(
                     alg_bytes / (sus["mean_period_us"] * 1e-6) / 1e9 / cg, 4)

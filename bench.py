@@ -585,13 +585,25 @@ def main():
         batch.launch_timed(kev[2 * k], kev[2 * k + 1])
     torch.cuda.synchronize()
     kern_ms = np.array([kev[2 * k].elapsed_time(kev[2 * k + 1]) for k in range(K)])
+    #  * isolated launches: every launch from an idle queue (synchronize after
+    #    each, as one synchronous shim call runs), an event before and after;
+    #    and beside them the same K launches with their event pairs queued
+    #    back to back (no synchronize): round 5's "isolated" pass, which each
+    #    launch's markers slow down instead
     iso = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
     for k in range(K):
         iso[2 * k].record(stream)
         step()
         iso[2 * k + 1].record(stream)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     iso_ms = [iso[2 * k].elapsed_time(iso[2 * k + 1]) for k in range(K)]
+    qev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
+    for k in range(K):
+        qev[2 * k].record(stream)
+        step()
+        qev[2 * k + 1].record(stream)
+    torch.cuda.synchronize()
+    qev_ms = [qev[2 * k].elapsed_time(qev[2 * k + 1]) for k in range(K)]
     #  * sustained: --sustained back-to-back launches (default 2000, ~0.13 s)
     #    with an event every 100, so drift from the short timed window to a
     #    long run shows as a series of segment periods
@@ -743,8 +755,14 @@ def main():
                                                 "the previous kernel's drain, so not used for frac",
                          "isolated_median_us": round(float(np.median(iso_ms)) * 1e3, 2),
                          "isolated_frac": round(alg_bytes / (float(np.median(iso_ms)) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "isolated_what": "untimed diagnostic: ordinary events before and after each launch (the "
-                                          "launch starts from an idle queue, as a single shim call does); median"},
+                         "isolated_what": "untimed diagnostic: ordinary events before and after each launch and a "
+                                          "synchronize after it (every launch starts from an idle queue, as a single "
+                                          "synchronous shim call does); median",
+                         "queued_event_pairs_median_us": round(float(np.median(qev_ms)) * 1e3, 2),
+                         "queued_event_pairs_what": "untimed diagnostic: the same K launches with their event pairs "
+                                                    "queued back to back, no synchronize between them (round 5's "
+                                                    "isolated pass): each launch's start waits on the markers of "
+                                                    "the one before (DESIGN.md section 4)"},
             "timing": {"what": "value = all ranks' blocks x K / the MAX over ranks of each rank's own elapsed "
                                "(from its start after the opening barrier + synchronize to its own synchronize "
                                "after the K launches); the closing barrier is outside it (barrier_after_ms); "

@@ -1,7 +1,8 @@
 """Summarise a rocprofv3 --kernel-trace run of bench.py: per-kernel-name
 launch durations (all launches), and the main kernel's launches split by
 bench phase in launch order -- the verification launch (1), warmup (W), timed
-(K), dispatch-event pass (K), isolated pass (K) -- after dropping the
+(K), dispatch-event pass (K), isolated pass (K), queued event-pair pass
+(K) -- after dropping the
 known-answer probe's small launches.
 Writes the JSON summary and, with a third path, a stats CSV of the timed
 phase alone (the launches bench.py's `value` and `roofline` time).
@@ -37,7 +38,8 @@ d = [(e - s) / 1e3 for s, e in se]
 P = 1  # bench.py's verification launch precedes the warmup
 bounds = {"verify": (0, P), "warmup": (P, P + warm), "timed": (P + warm, P + warm + steps),
           "dispatch_events": (P + warm + steps, P + warm + 2 * steps),
-          "isolated": (P + warm + 2 * steps, P + warm + 3 * steps)}
+          "isolated": (P + warm + 2 * steps, P + warm + 3 * steps),
+          "queued_event_pairs": (P + warm + 3 * steps, P + warm + 4 * steps)}
 out["main_kernel"] = main
 out["main_phases"] = {k: stats(d[a:b]) for k, (a, b) in bounds.items() if d[a:b]}
 a, b = bounds["timed"]

@@ -120,3 +120,36 @@ def test_multi_shapes_mask_and_streams(dev, port):
     cat = C.gather_dev(outs2, 0)
     torch.cuda.synchronize()
     assert np.array_equal(C.to_u32(cat), np.concatenate([port.fixed(host[o:], st, ln, n) for o, st, ln, n in specs[:3]]))
+
+
+@pytest.mark.gpu
+def test_config5_single_process_shards_full(dev, port):
+    """BASELINE config 5 in ONE process: 10^7 x 4 KiB blocks round-robin over
+    8 shards (the 8-GPU node's layout; on this box all on device 0, 41 GB),
+    every shard checksummed where it lies (nvl_crc32c_fixed_dev_multi), the
+    results gathered into config 5's global order (nvl_crc32c_gather_dev):
+    the golden first / last CRCs, digest and each shard's own digest
+    (tests/golden/configs.json cfg5, reference-pinned)."""
+    import torch
+    from conftest import load_golden
+    g = load_golden("configs")["cfg5"]
+    n, L, G = g["n"], g["len"], 8
+    free, _ = torch.cuda.mem_get_info(dev)
+    if free < n * L + (4 << 30):
+        pytest.skip(f"needs {n * L / 1e9:.0f} GB free HBM")
+    shards, bufs = [], []
+    for k in range(G):
+        nk = (n - k + G - 1) // G
+        b = torch.empty(nk * L, dtype=torch.uint8, device=dev)
+        C.fill_splitmix(b, nk, L, g["seed"], first_block=k, block_step=G)
+        bufs.append(b)
+        shards.append((b, L, L, nk))
+    outs = C.extend_fixed_multi(shards)
+    rr = C.to_u32(C.gather_dev(outs, 0, round_robin=True))
+    assert [int(x) for x in rr[:8]] == g["crc_first"]
+    assert int(rr[-1]) == g["crc_last"]
+    assert port.digest(rr) == g["digest"]
+    want = g["ranks"][str(G)]["rank_digests"]
+    assert [port.digest(C.to_u32(o)) for o in outs] == want
+    del bufs, shards, outs
+    torch.cuda.empty_cache()

@@ -49,17 +49,29 @@ def one(mode):
     clk = (s[:, 5] - s[:, 4]) / dt * 100.0  # MHz
     cnt = np.maximum((s[:, 3] & 0xFFFFFFFF).astype(np.float64), 1)
     end = (s[:, 2] - t0) / 100.0
+    wstart = ((s[:, 0] - t0) / 100.0).reshape(-1, 16).min(axis=1)  # each workgroup's first wave start
+    wend = end.reshape(-1, 16).max(axis=1)
+    one.starts.append(wstart)
+    one.ends.append(wend)
     return {"span_us": float(end.max()), "clock_mhz_p50": float(np.median(clk)), "clock_mhz_p10": float(np.percentile(clk, 10)),
             "fill_us_p50": float(np.median((s[:, 1] - s[:, 0]) / 100.0)),
             "us_per_unit_p50": float(np.median((s[:, 2] - s[:, 1]) / 100.0 / cnt)),
             "end_p50_us": float(np.median(end)), "start_spread_us": float((s[:, 0].max() - t0) / 100.0)}
 
 
+one.starts, one.ends = [], []
 launch(); torch.cuda.synchronize()
 for _ in range(300):  # the sustained state first
     launch()
 res = {}
 for mode in ("queued", "isolated", "queued", "isolated"):
+    one.starts, one.ends = [], []
     rows = [one(mode) for _ in range(int(os.environ.get("ITERS", "20")))]
-    res.setdefault(mode, []).append({k: round(float(np.median([r[k] for r in rows])), 2) for k in rows[0]})
+    r = {k: round(float(np.median([x[k] for x in rows])), 2) for k in rows[0]}
+    st_ = np.median(np.array(one.starts), axis=0)
+    en_ = np.median(np.array(one.ends), axis=0)
+    r["wg_start_us_by_id_32"] = [round(float(x), 2) for x in st_.reshape(-1, 32).mean(axis=1)]
+    r["wg_end_us_by_id_32"] = [round(float(x), 2) for x in en_.reshape(-1, 32).mean(axis=1)]
+    r["wg_start_vs_id_slope_us"] = round(float(np.polyfit(np.arange(st_.size) / st_.size, st_, 1)[0]), 2)
+    res.setdefault(mode, []).append(r)
 print(json.dumps(res))

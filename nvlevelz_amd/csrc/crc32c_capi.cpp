@@ -72,11 +72,6 @@ struct DeviceState {
   int status = NVL_CRC32C_OK;  // OK, or why the backend is unusable
   std::mutex cmu;
   std::unordered_map<hipStream_t, uint32_t*> counters;  // per-stream counter blocks
-  struct RouteAux {
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-  };
-  std::unordered_map<hipStream_t, RouteAux> aux;  // per-stream side stream of the routed calls
 };
 
 std::mutex g_mu;
@@ -119,70 +114,13 @@ uint32_t* counters_for(DeviceState* s, hipStream_t st) {
   return c;
 }
 
-void destroy_aux(const DeviceState::RouteAux& a) {
-  if (a.side) (void)hipStreamDestroy(a.side);
-  if (a.fork) (void)hipEventDestroy(a.fork);
-  if (a.join) (void)hipEventDestroy(a.join);
-}
-
-// The side stream and fork / join events of routed calls on `st`
-// (LaunchCtx::side, launch_routed's fork/join form): a non-blocking stream of
-// st's device, created on first use; false when unavailable (the call then
-// runs on `st` alone).  Lock-free after a thread's first routed call on a
-// stream, like counters_for.
-bool route_aux_for(DeviceState* s, hipStream_t st, LaunchCtx* lc) {
-  struct Cache {
-    uint64_t gen = 0;
-    DeviceState* s = nullptr;
-    hipStream_t st = nullptr;
-    DeviceState::RouteAux a;
-  };
-  thread_local Cache cache;
-  const uint64_t gen = g_generation.load(std::memory_order_acquire);
-  if (!(cache.gen == gen && cache.s == s && cache.st == st && cache.a.side)) {
-    std::lock_guard<std::mutex> lk(s->cmu);
-    auto it = s->aux.find(st);
-    DeviceState::RouteAux a;
-    if (it != s->aux.end()) {
-      a = it->second;
-    } else {
-      if (s->aux.size() >= kMaxCounterStreams) return false;
-      int prev = -1;
-      (void)hipGetDevice(&prev);
-      if (prev != s->device) (void)hipSetDevice(s->device);
-      bool ok = hipStreamCreateWithFlags(&a.side, hipStreamNonBlocking) == hipSuccess &&
-                hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&a.join, hipEventDisableTiming) == hipSuccess;
-      if (prev >= 0 && prev != s->device) (void)hipSetDevice(prev);
-      if (!ok) {
-        (void)hipGetLastError();
-        destroy_aux(a);
-        return false;
-      }
-      s->aux[st] = a;
-    }
-    cache = Cache{gen, s, st, a};
-  }
-  lc->side = cache.a.side;
-  lc->fork = cache.a.fork;
-  lc->join = cache.a.join;
-  return true;
-}
-
-// Drop the counter block and the routed calls' side stream of a stream that
-// is about to be destroyed (a later stream may get the same handle value; the
-// block is re-created zeroed).
+// Drop the counter block of a stream that is about to be destroyed (a later
+// stream may get the same handle value; the block is re-created zeroed).
 void forget_counter(int device, hipStream_t st) {
   if (device < 0 || device >= kMaxDevices) return;
   DeviceState* s = g_state[device].load(std::memory_order_acquire);
   if (!s) return;
   std::lock_guard<std::mutex> lk(s->cmu);
-  auto ia = s->aux.find(st);
-  if (ia != s->aux.end()) {
-    (void)hipStreamSynchronize(ia->second.side);
-    destroy_aux(ia->second);
-    s->aux.erase(ia);
-  }
   auto it = s->counters.find(st);
   if (it == s->counters.end()) return;
   (void)hipFree(it->second);
@@ -338,7 +276,6 @@ int do_batch(DeviceState* s, const void* base, const uint64_t* offsets, const ui
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr};
   const bool small = var_plan_small(n);
   if (s->num_cu <= 1023) lc.counter = counters_for(s, st);
-  if (lc.counter && routed) (void)route_aux_for(s, st, &lc);
   if (lc.counter) {  // (cs holds lpre, the unit map region the tiles)
     hipError_t ef =
         routed ? launch_routed(lc, static_cast<const uint8_t*>(base), 0, true, offsets, lengths, n, init, init_all, out,
@@ -383,7 +320,6 @@ int do_region(DeviceState* s, const void* region, uint64_t region_len, const uin
   LaunchCtx lc{st, s->num_cu, s->tables, nullptr, ev_start, ev_stop};
   if (checked && s->num_cu <= 1023) lc.counter = counters_for(s, st);
   checked = checked && lc.counter;
-  if (checked) (void)route_aux_for(s, st, &lc);
   const BatchWs L = batch_ws(n, s->num_cu, region_cap_chunks(region_len));
   const size_t need = checked ? L.total : region_ws_bytes(region_len, n);
   bool own = false;
@@ -771,10 +707,6 @@ int nvl_crc32c_shutdown(void) {
         (void)hipSetDevice(d);
         (void)hipFree(s->tables);
         for (auto& kv : s->counters) (void)hipFree(kv.second);
-        for (auto& kv : s->aux) {
-          (void)hipStreamSynchronize(kv.second.side);
-          destroy_aux(kv.second);
-        }
         if (prev >= 0) (void)hipSetDevice(prev);
       }
       delete s;

@@ -52,11 +52,6 @@ struct LaunchCtx {
   // kernels alone and add no marker packet between back-to-back launches.
   hipEvent_t ev_start = nullptr;
   hipEvent_t ev_stop = nullptr;
-  // Routed calls: a side stream of the same device with its fork / join
-  // events (launch_routed's fork/join form); nullptr: one stream.
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr;
-  hipEvent_t join = nullptr;
 };
 
 void build_device_tables(uint32_t* words /* kTableWords */);

@@ -134,49 +134,6 @@ __global__ __launch_bounds__(kThreads, 1) void crc32c_route_kernel(RegionGeom rg
   }  // (the page path runs in crc32c_var_fused_kernel: here its registers would spill the region path's SGPRs)
 }
 
-// The fork/join form of a routed call (launch_routed with a side stream):
-// after the plan, the caller's stream runs crc32c_route_region_kernel -- the
-// region path, or an immediate return -- while a side stream runs
-// crc32c_route_heads_kernel (the verdict word for the body kernel, and the
-// head kernel's work when the batch takes the batch path) and then the body
-// kernel; the caller's stream waits for the side stream at the end.  On the
-// region path the two small kernels' early exits run beside the region
-// kernel instead of after it (the body kernel's exit alone
-// cost ~2 us of every routed call), and the region path's kernel carries no
-// head-path code (the combined kernel's scalar spills).
-__global__ __launch_bounds__(kThreads, 1) void crc32c_route_region_kernel(RegionGeom rg, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRLdsBytes];
-  uint64_t lo, hi;
-  if (!route_region(ka.route, lo, hi)) return;
-  if (ka.route.dyn) {
-    const uintptr_t base = (uintptr_t)ka.route.base, start = base + lo;
-    const uintptr_t O = start & ~(uintptr_t)(kChunk - 1u);
-    rg.grid = reinterpret_cast<const uint8_t*>(O);
-    rg.rel0 = (uint64_t)(base - O);  // (wrapping: buffer i at rel0 + offsets[i] >= start - O)
-    rg.rs = (uint64_t)(start - O);
-    rg.re = (uint64_t)(base + hi - O);
-    rg.nc = (rg.re + kChunk - 1u) / kChunk;
-  }
-  const uint64_t gw = (rg.nc + kWavesPerWG - 1u) / kWavesPerWG;  // (the host's grid_for)
-  const uint32_t G = (uint32_t)max<uint64_t>(1u, min<uint64_t>(gridDim.x, gw));
-  if (blockIdx.x >= G) return;
-  run_region<kFastU>(rg, ka, lds, G);
-}
-
-__global__ __launch_bounds__(kThreads, 1) void crc32c_route_heads_kernel(VarGeom vg, KArgs ka) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kHeadLdsBytes];
-  uint64_t lo, hi;
-  uint64_t* const verdict = &const_cast<RoutePart*>(ka.route.parts)[kRoutePlanMax].bad;
-  if (route_region(ka.route, lo, hi)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *verdict = kRouteRegion;
-    return;
-  }
-  const int kind = route_other(ka.route);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *verdict = (uint64_t)kind;
-  if (kind != kRouteHeads || blockIdx.x >= ka.tile_G) return;
-  run_heads(vg, ka, lds);
-}
-
 }  // namespace dev
 
 // A process-wide call generation (never 0, the zeroed workspace's value),
@@ -256,33 +213,16 @@ hipError_t launch_routed(const LaunchCtx& lc, const uint8_t* base, uint64_t regi
   ka.tile_S = (n + hg - 1) / hg;
   ka.short_ok = 1u;
   ka.route = rt;
+  hipLaunchKernelGGL(dev::crc32c_route_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kThreads), 0, lc.stream, rg, vg,
+                     ka);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
   dev::KArgs kf{out, flags, recs, lc.tables, lc.counter, hc};
   kf.lpre = lpre;
   kf.tiles = tiles;
   kf.tile_G = hg;
   kf.tile_S = ka.tile_S;
   kf.route = rt;
-  if (lc.side && lc.fork && lc.join) {
-    // fork/join: region path here, heads + body on the side stream
-    if ((e = hipEventRecord(lc.fork, lc.stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(dev::crc32c_route_region_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kThreads), 0, lc.stream,
-                       rg, ka);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(lc.side, lc.fork, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(dev::crc32c_route_heads_kernel, dim3(hg), dim3(dev::kThreads), 0, lc.side, vg, ka);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    LaunchCtx ls = lc;
-    ls.stream = lc.side;
-    ls.ev_start = ls.ev_stop = nullptr;
-    if ((e = launch_var_body(ls, vg, kf)) != hipSuccess) return e;
-    if ((e = hipEventRecord(lc.join, lc.side)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(lc.stream, lc.join, 0)) != hipSuccess) return e;
-    return lc.ev_stop ? hipEventRecord(lc.ev_stop, lc.stream) : hipSuccess;
-  }
-  hipLaunchKernelGGL(dev::crc32c_route_kernel, dim3((uint32_t)lc.num_cu), dim3(dev::kThreads), 0, lc.stream, rg, vg,
-                     ka);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
   return launch_var_body(lc, vg, kf);
 }
 

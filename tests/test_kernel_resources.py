@@ -51,8 +51,7 @@ def _parse(stderr, kernels):
 
 HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_fixed_long_kernel", "crc32c_var_kernel", "crc32c_var_fused_kernel",
        "crc32c_region_kernel", "crc32c_chunks_kernel",
-       "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel", "crc32c_route_kernel", "crc32c_route_plan",
-       "crc32c_route_region_kernel", "crc32c_route_heads_kernel"]
+       "crc32c_plan_small", "crc32c_fixup_kernel", "crc32c_head_kernel", "crc32c_route_kernel", "crc32c_route_plan"]
 # SGPR spills go to VGPR lanes (v_writelane/v_readlane), not memory: a bound
 # per kernel so that a jump shows.  The fused kernel parks plan-phase scalars
 # there; the variable-length kernels keep scheduler C's two chunk positions
@@ -60,7 +59,7 @@ HOT = ["crc32c_fixed_kernelILi0", "crc32c_fixed_kernelILi1", "crc32c_fixed_long_
 # metadata (current, next) live in SGPRs while the next-but-one's loads are in
 # flight.
 SGPR_SPILL_MAX = {"crc32c_var_fused_kernel": 48, "crc32c_var_kernel": 48, "crc32c_head_kernel": 160,
-                  "crc32c_route_kernel": 48, "crc32c_route_heads_kernel": 160}  # (the head kernel's and the region kernel's scalars in one kernel)
+                  "crc32c_route_kernel": 48}  # (the head kernel's and the region kernel's scalars in one kernel)
 
 
 @pytest.mark.parametrize("name", HOT)
@@ -84,7 +83,7 @@ def test_region_fold_claim_placement(usage):
     # run_region runs in crc32c_region_kernel (the one-launch form) and in
     # crc32c_route_kernel (the routed region_dev / batch_dev default, ADVICE
     # r05): both must keep the 4-waves-per-SIMD placement.
-    for name in ("crc32c_region_kernel", "crc32c_route_kernel", "crc32c_route_region_kernel"):
+    for name in ("crc32c_region_kernel", "crc32c_route_kernel"):
         hits = [k for k in usage if name in k]
         assert hits, name
         for k in hits:

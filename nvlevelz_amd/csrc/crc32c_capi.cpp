@@ -59,13 +59,6 @@ void build_device_tables(uint32_t* w) {
     for (uint32_t n = 0; n < 8; ++n)
       for (uint32_t v = 0; v < 16; ++v) w[kTabNib + (n * 16u + v) * 64u + j] = gf_mul(m, v << (4u * n));
   }
-  // powers of the shift by one chunk, x^(8 * 4096 k), for the cooperative
-  // fold of long region buffers (run_region's long mode)
-  uint32_t xc = kOne;
-  for (uint32_t k = 0; k < kXcLen; ++k) {
-    w[kTabXc + k] = xc;
-    xc = gf_mul(xc, w[kTabXp8 + 4096]);
-  }
 }
 
 namespace {

@@ -451,90 +451,6 @@ __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds
   return true;
 }
 
-// The cooperative fold of a workgroup of long buffers (run_region's long
-// mode; config 3's buffers average eight chunks).  Folded one lane per
-// buffer, a buffer's middle chunks are a chain of dependent shifts by 4096
-// bytes (two nibble-column rounds each) and a workgroup's ~128 buffers fill
-// two 64-lane slices -- two of its sixteen waves: 5.3-5.7 us of arithmetic
-// (DESIGN.md §8 item 0).  Here every wave folds 8-buffer slices, lane
-// 8b + q taking run q of buffer b's items (item 0: the head term at chunk
-// c0's end, item t > 0: chunk c0 + t's raw): the run's Horner P times
-// x^(8 * 4096 * (nit - end + 1)) (the blob's xc table), an XOR over the 8
-// lanes, finished by lane q = 0 -- fold_out's longer branch, split 8 ways
-// (tests/test_math.py::test_region_long_fold_runs).  One phase: every
-// lane's metadata, quads and powers (fold_in) are loaded before the fold
-// barrier like the per-lane fold's, its raws and records right after it,
-// all together.  (Round 5's form deferred only the long buffers to a second
-// phase whose inputs were dependent round trips: slower)
-// Buffers of at most two chunks, longer than kXcLen - 1 items, outside the
-// region or without their records go through lane q = 0's per-lane fold.
-constexpr uint32_t kLongAvg = 3;  // long mode: the owned buffers average >= 3 chunks
-__device__ __forceinline__ void fold_long(const RegionGeom& g, const KArgs& ka, const uint8_t* lds, const uint8_t* lsl,
-                                          const LaneBase& lb, int lane, uint32_t wv, uint64_t ib, uint64_t ib1,
-                                          uint64_t c0w, uint64_t B1) {
-  const uint32_t q = (uint32_t)lane & 7u;
-  const uint64_t nsl8 = (ib1 - ib + 7u) / 8u;
-  uint64_t k8 = wv;
-  FoldIn f;
-  if (k8 < nsl8) f = fold_in(g, ka.tables, min(ib + 8u * k8 + (uint64_t)(lane >> 3), ib1 - 1u), c0w, B1);
-  __syncthreads();  // every unit's raws and records are written
-  while (k8 < nsl8) {
-    const uint64_t i = ib + 8u * k8 + (uint64_t)(lane >> 3);
-    const bool valid = i < ib1;
-    uint4 q_s = make_uint4(0u, 0u, 0u, 0u), q_e = q_s;
-    uint32_t part = 0u;
-    bool coop = false;
-    uint64_t c0 = 0, c1 = 0;
-    uint32_t os = 0, oe = kChunk;
-    if (valid && f.fast) {
-      const uint64_t s = f.s, e = f.s + f.L;
-      c0 = s >> 12;
-      c1 = (e - 1u) >> 12;
-      os = (uint32_t)(s & (kChunk - 1u));
-      oe = (uint32_t)(e - (c1 << 12));
-      q_s = g.qs[i];
-      q_e = g.qe[i];
-      const uint32_t nit = (uint32_t)min<uint64_t>(c1 - c0, kXcLen);
-      const uint32_t a = (nit * q + 7u) / 8u, b = (nit * (q + 1u) + 7u) / 8u;  // (run 0 holds item 0)
-      uint32_t rr[4];  // this lane's raws, loaded together (runs of <= 8 items)
-#pragma unroll
-      for (uint32_t t = 0; t < 4u; ++t) rr[t] = g.raws[c0 + min(a + t, nit ? nit - 1u : 0u)];  // (inside [c0, c1])
-      const bool recs = !((os && (q_s.z != g.gen || q_s.w != (uint32_t)i)) ||
-                          (oe != kChunk && (q_e.z != g.gen || q_e.w != (uint32_t)i)));
-      coop = recs && c1 >= c0 + 2u && c1 - c0 < (uint64_t)kXcLen;
-      if (coop && b > a) {
-        uint32_t P = rr[0];
-        if (q == 0u) {  // item 0: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) ^ raw c0, T = R(s) ^ ~init
-          const uint32_t T = (os ? quad_prefix_lds(lsl, lb, q_s.y, f.vs, s & 63u) : 0u) ^ f.ninit;
-          P = (os ? q_s.x : 0u) ^ gf_mul_lds(lsl, lb, f.xs, T) ^ rr[0];
-        }
-#pragma unroll
-        for (uint32_t t = 1; t < 4u; ++t)
-          if (a + t < b) P = sh4096_lds(lds, P, lane) ^ rr[t];
-        for (uint32_t t = a + 4u; t < b; ++t) P = sh4096_lds(lds, P, lane) ^ g.raws[c0 + t];  // (runs > 4: nit > 32)
-        part = gf_mul_lds(lsl, lb, ka.tables[kTabXc + (nit - b + 1u)], P);
-      }
-    }
-    part ^= dpp_xor1(part);  // (every lane: the XOR over each group of 8)
-    part ^= dpp_xor2(part);
-    part ^= swz_xor4(part);
-    if (valid && q == 0u) {
-      uint32_t v = 0u;
-      if (coop) {
-        const uint64_t e = f.s + f.L;
-        const uint32_t ze = oe == kChunk ? g.raws[c1] : q_e.x;
-        const uint32_t re = oe == kChunk ? 0u : quad_prefix_lds(lsl, lb, q_e.y, f.ve, e & 63u);
-        v = gf_mul_lds(lsl, lb, f.xe, part ^ ze) ^ re;
-      } else if (!(f.fast && fold_out(g, lds, lsl, lb, lane, f, q_s, q_e, (uint32_t)i, v))) {
-        v = serial_raw(ka.tables + kGSlice, f.ninit, g.grid + f.s, f.L);  // (outside the region too: the caller's memory)
-      }
-      ka.out[i] = finish(~v, ka.flags);
-    }
-    k8 += kWavesPerWG;
-    if (k8 < nsl8) f = fold_in(g, ka.tables, min(ib + 8u * k8 + (uint64_t)(lane >> 3), ib1 - 1u), c0w, B1);
-  }
-}
-
 // LDS slots in the region image's lane-63 column (never read by the lane
 // shifts): row r at r * 256 + 252.  Row 16 (T[1][0][63]) is 0 in the blob.
 // (generic pointer: the volatile accesses become flat loads, which count in
@@ -774,11 +690,6 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   const uint64_t ib = ((uint64_t)*region_slot(lds, kSlotOwnHi) << 32) | *region_slot(lds, kSlotOwnLo);
   const uint64_t ib1 = ((uint64_t)*region_slot(lds, kSlotEndHi) << 32) | *region_slot(lds, kSlotEndLo);
   const uint64_t c0w = B0 - *region_slot(lds, kSlotHalo);  // the first chunk streamed here
-  if (ib1 > ib && B1 - c0w >= (uint64_t)kLongAvg * (ib1 - ib)) {  // (uniform: LDS slots and the range)
-    fold_long(g, ka, lds, lds + (kRSliceOff - kSliceOff), lb, lane, wv, ib, ib1, c0w, B1);
-    NVL_TL_END();
-    return;
-  }
   const uint64_t nsl = ib1 > ib ? (ib1 - ib + 63u) / 64u : 0u;
   // slices k = s (mod 4) go to the waves on SIMD s: the fold is VALU-bound,
   // so a SIMD holding two folding waves finishes last.  A SIMD that holds

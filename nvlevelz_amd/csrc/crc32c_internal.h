@@ -26,10 +26,7 @@ namespace nvl {
 constexpr uint32_t kXp8Len = 8193;  // a buffer spanning at most two chunks has at most 8192 bytes
 constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + kXp8Len;
 constexpr uint32_t kTabNib = (kTabXm8 + 4096u + 3u) & ~3u;
-//   [28740,28804) xc[64]              x^(8 * 4096 k) mod P, k = 0..63   (region fold, long buffers)
-constexpr uint32_t kXcLen = 64;
-constexpr uint32_t kTabXc = kTabNib + 8u * 16u * 64u;
-constexpr uint32_t kTableWords = kTabXc + kXcLen;
+constexpr uint32_t kTableWords = kTabNib + 8u * 16u * 64u;
 
 // A portion of one buffer processed inside one work unit (fix-up input).
 struct Rec {

@@ -59,6 +59,11 @@ void build_device_tables(uint32_t* w) {
     for (uint32_t n = 0; n < 8; ++n)
       for (uint32_t v = 0; v < 16; ++v) w[kTabNib + (n * 16u + v) * 64u + j] = gf_mul(m, v << (4u * n));
   }
+  // the region fold's chunk shifts: by 4096, 8192, 12288 and 16384 bytes
+  for (uint32_t d = 1; d <= 4; ++d) {
+    build_shift_op(pw.x2n, 4096ull * d, op);
+    memcpy(w + kTabShc + (d - 1u) * 1024u, op, sizeof(op));
+  }
 }
 
 namespace {

@@ -875,6 +875,9 @@ __device__ __forceinline__ void build_words(const BufInfo& bi, uint32_t c, int l
 // workgroup's unit counter.  The slice replicas follow at 32 KiB.
 constexpr uint32_t kRNibOff = 0;
 constexpr uint32_t kRCtrOff = 252;  // T[0][0][63]
+// The fold's chunk shifts (the blob's shc tables, 16 KiB) over the nibble
+// tables' rows 64..127, written once the workgroup's chunks are done.
+constexpr uint32_t kRShcOff = 16384;
 constexpr uint32_t kRSliceOff = 32768;
 constexpr uint32_t kRLdsBytes = kRSliceOff + kRepBytes;  // 163840 B
 static_assert(kRLdsBytes <= 160u * 1024u, "region LDS image exceeds 160 KiB");
@@ -914,8 +917,12 @@ __device__ __forceinline__ void fill_region_store(uint8_t* lds, const RegionFill
 #pragma unroll
   for (int q = 0; q < (int)(2048 / kThreads); ++q) {
     uint4 v = f.nib[q];
-    if (t + q * (int)kThreads == (int)(kRCtrOff >> 4)) v.w = ctr0;  // units 0..ctr0-1 are pre-assigned
-    dst[t + q * (int)kThreads] = v;
+    // column 63 of rows 0..15 holds the unit counter (units 0..ctr0-1 are
+    // pre-assigned) and the workgroup's slots (crc32c_dev_region.h), zeroed
+    // here; the lane shifts never read that column
+    const int gi = t + q * (int)kThreads;
+    if (gi < 256 && (gi & 15) == 15) v.w = gi == (int)(kRCtrOff >> 4) ? ctr0 : 0u;
+    dst[gi] = v;
   }
 }
 static_assert(8192 % kThreads == 0 && 2048 % kThreads == 0, "region fill: whole rounds per thread");

@@ -390,27 +390,16 @@ __device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* lsl, const LaneBas
   return p;
 }
 
-// shift(v, 64 (63 - j)) through column j of the nibble tables (jb = 4j).
-__device__ __forceinline__ uint32_t col_shift(const uint8_t* lds, uint32_t v, uint32_t jb) {
-  const uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
-  const uint8_t* nb = lds + kRNibOff;
-  const uint32_t r0 = lds_u32(nb + 0u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0400u));
-  const uint32_t r1 = lds_u32(nb + 1u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0400u));
-  const uint32_t r2 = lds_u32(nb + 2u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0500u));
-  const uint32_t r3 = lds_u32(nb + 3u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0500u));
-  const uint32_t r4 = lds_u32(nb + 4u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0600u));
-  const uint32_t r5 = lds_u32(nb + 5u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0600u));
-  const uint32_t r6 = lds_u32(nb + 6u * 4096u, __builtin_amdgcn_perm(lo, jb, 0x0C0C0700u));
-  const uint32_t r7 = lds_u32(nb + 7u * 4096u, __builtin_amdgcn_perm(hi, jb, 0x0C0C0700u));
-  return xor3(xor3(r0, r1, r2), xor3(r3, r4, r5), r6) ^ r7;
-}
-
-// shift(acc, 4096) as two column shifts, 64 a and 64 (64 - a) bytes with
-// a = (lane & 31) + 1: the 32 lanes of a half read 32 distinct columns
-// (banks) -- one shared column would serialise them.
-__device__ __forceinline__ uint32_t sh4096_lds(const uint8_t* lds, uint32_t acc, int lane) {
-  const uint32_t a = ((uint32_t)lane & 31u) + 1u;
-  return col_shift(lds, col_shift(lds, acc, (63u - a) << 2), (a - 1u) << 2);
+// shift(v, 4096 d) for d = 1..4 from the fold's byte-sliced tables (tab =
+// (d - 1) * 4096, per lane): one level of four lookups (one copy: bank
+// conflicts, but half the fold's LDS reads and a quarter of its VALU of the
+// two dependent nibble-column shifts it replaces, which measured the same on
+// r / v and 1.2 us slower on config 3).  Valid after the fold's table copy.
+__device__ __forceinline__ uint32_t shc_lds(const uint8_t* lds, uint32_t v, uint32_t tab) {
+  const uint8_t* b = lds + kRShcOff;
+  const uint32_t a0 = ((v & 255u) << 2) + tab, a1 = (((v >> 8) & 255u) << 2) + tab;
+  const uint32_t a2 = (((v >> 16) & 255u) << 2) + tab, a3 = ((v >> 24) << 2) + tab;
+  return xor3(lds_u32(b, a0), lds_u32(b + 1024u, a1), lds_u32(b + 2048u, a2)) ^ lds_u32(b + 3072u, a3);
 }
 
 __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds, const uint8_t* lsl,
@@ -431,28 +420,44 @@ __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds
     // or shift4096(Qe(s) ^ raw c0) (two) -- ^ Ze, unshifted to e, and T
     // straight to e:  (X ^ Ze) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e)
     // (for two chunks x^(-8(4096 - oe)) x^(8(8192 - os)) = x^(8L))
-    const uint32_t sh = sh4096_lds(lds, qs ^ r0, lane);
+    const uint32_t sh = shc_lds(lds, qs ^ r0, 0u);
     v = gf_mul_lds(lsl, lb, f.xe, (c1 == c0 ? qs : sh) ^ ze) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ re;
     return true;
   }
-  // Longer: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) at chunk c0's end, the chunks in between, unshifted from c1's end
+  // Longer: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) at chunk c0's end, then up
+  // to four chunks per step -- acc at chunk c + k's end = shift(acc, 4096 k)
+  // ^ the raws of chunks c + 1 .. c + k below c1, each shifted by its own
+  // distance (independent of acc: one dependent lookup level per step) --,
+  // unshifted from c1's end.  The next step's raws are in flight meanwhile.
+  (void)rm;
   uint32_t acc = qs ^ gf_mul_lds(lsl, lb, f.xs, T) ^ r0;
-  acc = sh4096_lds(lds, acc, lane) ^ rm;
-  for (uint64_t c = c0 + 2u; c < c1; c += 4u) {  // further chunks in between, four loads at a time
-    uint32_t rr[4];
+  uint32_t rr[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) rr[k] = g.raws[min(c + (uint64_t)k, c1)];
+  for (int j = 0; j < 4; ++j) rr[j] = g.raws[min(c0 + 1u + (uint64_t)j, c1 - 1u)];
+  for (uint64_t c = c0; c < c1;) {
+    const uint32_t k = (uint32_t)min(c1 - c, (uint64_t)4);
+    const uint64_t cn = c + k;
+    uint32_t rn[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c + (uint64_t)k < c1) acc = sh4096_lds(lds, acc, lane) ^ rr[k];
+    for (int j = 0; j < 4; ++j) rn[j] = g.raws[min(cn + 1u + (uint64_t)j, c1 - 1u)];
+    uint32_t x = shc_lds(lds, acc, (k - 1u) << 12);
+#pragma unroll
+    for (uint32_t j = 1; j <= 4u; ++j) {  // chunk c + j: below c1 iff c + j < c1 (then j <= k)
+      const uint32_t rj = c + j < c1 ? rr[j - 1u] : 0u;
+      x ^= j < k ? shc_lds(lds, rj, (k - j - 1u) << 12) : rj;  // (j > k: rj = 0)
+    }
+    acc = x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rr[j] = rn[j];
+    c = cn;
   }
-  acc = sh4096_lds(lds, acc, lane);
   v = gf_mul_lds(lsl, lb, f.xe, acc ^ ze) ^ re;
   return true;
 }
 
 // LDS slots in the region image's lane-63 column (never read by the lane
-// shifts): row r at r * 256 + 252.  Row 16 (T[1][0][63]) is 0 in the blob.
+// shifts): row r at r * 256 + 252, rows 0..15, zeroed by the fill (rows
+// 64..127 take the fold's chunk-shift tables once the chunks are done).
 // (generic pointer: the volatile accesses become flat loads, which count in
 // vmcnt as well; an LDS-qualified pointer was measured slower, see load_unit)
 typedef volatile uint32_t lds_vu32;
@@ -460,9 +465,9 @@ __device__ __forceinline__ lds_vu32* region_slot(uint8_t* lds, uint32_t r) {
   return (lds_vu32*)(lds + kRNibOff + r * 256u + 252u);
 }
 constexpr uint32_t kSlotOwnLo = 1, kSlotOwnHi = 2, kSlotEndLo = 3, kSlotEndHi = 4, kSlotHalo = 5;
-// (rows 16, 32, 48, 64, 80, 96: T[n][0][63] = 0 in the blob; row 96 counts the
-// workgroup's waves per SIMD, one byte each)
-constexpr uint32_t kSlotReady = 16, kSlotTail = 32, kSlotWaves = 96;
+// (row 6: the halo published; rows 7..10: the fold's slice counters per SIMD;
+// row 11 counts the workgroup's waves per SIMD, one byte each)
+constexpr uint32_t kSlotReady = 6, kSlotTail = 7, kSlotWaves = 11;
 
 // Scheduler A over the region's chunks, and the per-buffer fold in the same
 // launch.  Workgroup b owns the chunk range [B0, B1) and the buffers
@@ -701,13 +706,17 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
   auto claim = [&]() -> uint64_t {
     uint32_t v = 0;
     if (lane == 0)
-      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail + 16u * cs)), 1u,
+      v = __hip_atomic_fetch_add(const_cast<uint32_t*>(region_slot(lds, kSlotTail + cs)), 1u,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return (uint64_t)cs + 4u * (uint64_t)uniform_u32(v);
   };
   uint64_t k = claim();
   FoldIn f;
   if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
+  const uint4 shc = reinterpret_cast<const uint4*>(ka.tables + kTabShc)[threadIdx.x];  // 16 KiB: one per thread
+  static_assert(kTabShc % 4u == 0 && 4u * 1024u == 4u * (uint32_t)kThreads, "fold tables: one uint4 per thread");
+  __syncthreads();  // every unit done: the nibble tables are free
+  reinterpret_cast<uint4*>(lds + kRShcOff)[threadIdx.x] = shc;
   __syncthreads();
   NVL_TL(3);
   const uint8_t* lsl = lds + (kRSliceOff - kSliceOff);

@@ -23,10 +23,13 @@ namespace nvl {
 //   [20548,28740)  nib[8][16][64]     T[n][v][j] = shift(v << 4n, 64(63 - j))  (region kernel:
 //                                     lane j's piece raw to the chunk end; 16-byte aligned, copied
 //                                     verbatim into LDS)
+//   [28740,32836) shc[4][4][256]     shift by 4096 d bytes (d = 1..4), byte-sliced (region fold: copied
+//                                     into LDS over the nibble tables' upper half once the chunks are done)
 constexpr uint32_t kXp8Len = 8193;  // a buffer spanning at most two chunks has at most 8192 bytes
 constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + kXp8Len;
 constexpr uint32_t kTabNib = (kTabXm8 + 4096u + 3u) & ~3u;
-constexpr uint32_t kTableWords = kTabNib + 8u * 16u * 64u;
+constexpr uint32_t kTabShc = kTabNib + 8u * 16u * 64u;
+constexpr uint32_t kTableWords = kTabShc + 4u * 1024u;
 
 // A portion of one buffer processed inside one work unit (fix-up input).
 struct Rec {

@@ -201,8 +201,10 @@ def test_region_path_model(port, seed):
         p += L + rng.choice([0, 0, 4, 5, 1, 64 - (p + L) % 64])
     # starts/ends exactly on piece and chunk boundaries; two whole chunks
     # (L = 8192: the longest buffer the direct fold takes); three chunks
-    bufs += [(4096, 64), (4096 * 2 - 64, 64 + 4096), (4096, 8192), (100, 8192), (4095, 4098)]
-    inits += [0, 7, 3, 0, 9]
+    # and the long fold's steps of up to four chunks: 3..12 chunks, chunk-aligned ends too
+    bufs += [(4096, 64), (4096 * 2 - 64, 64 + 4096), (4096, 8192), (100, 8192), (4095, 4098),
+             (17, 4096 * 5), (4096, 4096 * 5), (300, 4096 * 9 + 77), (5, 4096 * 12 - 5), (4100, 4096 * 4 + 8)]
+    inits += [0, 7, 3, 0, 9, 1, 2, 0, 5, 6]
     got = km.region_batch(mem, bufs, inits)
     want = [port.extend(i, mem[s:s + L]) for (s, L), i in zip(bufs, inits)]
     assert got == want

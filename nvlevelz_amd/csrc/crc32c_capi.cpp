@@ -64,6 +64,13 @@ void build_device_tables(uint32_t* w) {
     build_shift_op(pw.x2n, 4096ull * d, op);
     memcpy(w + kTabShc + (d - 1u) * 1024u, op, sizeof(op));
   }
+  // x^(8*4096*q): q chunks' worth of x^8 (the long fold's x^(8L) = x^(8 (L mod 4096)) x^(8*4096*q) ...)
+  const uint32_t c4k = w[kTabXp8 + 4096];
+  uint32_t a = kOne;
+  for (uint32_t q = 0; q < 256; ++q) {
+    w[kTabPw4k + q] = a;
+    a = gf_mul(a, c4k);
+  }
 }
 
 namespace {

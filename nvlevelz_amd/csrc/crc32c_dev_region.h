@@ -313,6 +313,38 @@ __device__ __forceinline__ uint32_t fold_sh4096(const uint32_t* sh, uint32_t acc
   return sh[acc & 255u] ^ sh[256u + ((acc >> 8) & 255u)] ^ sh[512u + ((acc >> 16) & 255u)] ^ sh[768u + (acc >> 24)];
 }
 
+// gf_mul(a, b) (crc32c_math.h) by bytes of a, Horner in x^8: with
+// B_j = b x^j (j < 8), C_k = sum_j a_{8k+j} B_j, a b = C_0 ^ x^8 (C_1 ^ x^8 (C_2
+// ^ x^8 C_3)), and v x^8 = T0[v & 255] ^ v >> 8 -- one LDS lookup (slice
+// table 0's replica) per byte instead of eight shift-reduce steps.  Bit
+// 31 - i of a is its x^i coefficient (reflected).
+__device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* lsl, const LaneBase& lb, uint32_t a, uint32_t b) {
+  uint32_t B[8];
+  B[0] = b;
+#pragma unroll
+  for (int j = 1; j < 8; ++j)
+    B[j] = (B[j - 1] >> 1) ^ ((uint32_t)__builtin_amdgcn_sbfe((int)B[j - 1], 0, 1) & kPolyReflected);
+  const uint8_t* sl = lsl + kSliceOff;
+  uint32_t p = 0u;
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {
+    if (k < 3) p = lds_u32(sl, __builtin_amdgcn_perm(p, lb.t0, 0x0C020400u)) ^ (p >> 8);  // p x^8
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p ^= (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - (8 * k + j), 1) & B[j];
+  }
+  return p;
+}
+
+// x^(8L) for a buffer longer than two chunks: x^(8 (L mod 4096)) x^(8*4096*(q mod 256))
+// (tables) and x^(2^(23 + b)) for every bit b of q >> 8, q = L div 4096.
+__device__ uint32_t xpow8_long(const uint32_t* tables, const uint8_t* lsl, const LaneBase& lb, uint64_t L) {
+  uint32_t p = gf_mul_lds(lsl, lb, tables[kTabXp8 + (L & (kChunk - 1u))], tables[kTabPw4k + ((L >> 12) & 255u)]);
+  uint32_t b = 23;
+  for (uint64_t q = L >> 20; q; q >>= 1, ++b)
+    if (q & 1u) p = gf_mul_lds(lsl, lb, p, tables[kGX2n + b]);
+  return p;
+}
+
 // The fold of one region buffer, in two halves.  fold_in: what depends on
 // the batch alone -- its metadata, the two 16-byte quads re-read for the
 // piece prefixes R (the end's clamped into the grid when it is a chunk end),
@@ -323,12 +355,12 @@ __device__ __forceinline__ uint32_t fold_sh4096(const uint32_t* sh, uint32_t acc
 // caller then checksums the buffer serially.
 struct FoldIn {
   uint64_t s, L;
-  uint32_t ninit, xs, xe, xt;  // x^(8(4096 - os)), x^(-8(4096 - oe)), x^(8L) (one or two chunks)
+  uint32_t ninit, xe, xt;  // x^(-8(4096 - oe)), x^(8L)
   u32x4 vs, ve;
   bool fast;  // inside the region, >= kRegionDirect bytes, every chunk streamed by this workgroup
 };
-__device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* tables, uint64_t i, uint64_t c0w,
-                                          uint64_t B1) {
+__device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* tables, const uint8_t* lsl,
+                                          const LaneBase& lb, uint64_t i, uint64_t c0w, uint64_t B1) {
   FoldIn f;
   const uint64_t off = ldg64(g.offsets, i), L = ldg64(g.lengths, i);
   f.ninit = ~(g.init ? g.init[i] : g.init_all);
@@ -338,13 +370,13 @@ __device__ __forceinline__ FoldIn fold_in(const RegionGeom& g, const uint32_t* t
   f.fast = inside && L >= kRegionDirect && (f.s >> 12) >= c0w && ((f.s + L - 1u) >> 12) < B1;
   const uint64_t s = f.fast ? f.s : 0u, e = f.fast ? f.s + L : 64u;  // (the grid's first chunk otherwise)
   const uint64_t c1 = (e - 1u) >> 12;
-  const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
+  const uint32_t oe = (uint32_t)(e - (c1 << 12));  // in [1, 4096]
   f.vs = ld16c((uintptr_t)g.grid + (s & ~(uint64_t)15));
   f.ve = ld16c((uintptr_t)g.grid + (oe == kChunk ? e - 16u : (e & ~(uint64_t)15)));
-  f.xs = tables[kTabXp8 + kChunk - os];
   f.xe = tables[kTabXm8 + (kChunk - oe)];
-  const uint64_t c0 = s >> 12;
-  f.xt = tables[kTabXp8 + (c1 <= c0 + 1u ? e - s : 0u)];  // (L <= 8192 there)
+  const uint64_t d = e - s;  // (L, or 64 for a buffer the fold checksums serially)
+  f.xt = tables[kTabXp8 + min(d, (uint64_t)(kXp8Len - 1u))];
+  if (d >= kXp8Len) f.xt = xpow8_long(tables, lsl, lb, d);  // longer than two chunks: metadata only
   return f;
 }
 
@@ -368,28 +400,6 @@ __device__ __forceinline__ uint32_t quad_prefix_lds(const uint8_t* lsl, const La
   return crc;
 }
 
-// gf_mul(a, b) (crc32c_math.h) by bytes of a, Horner in x^8: with
-// B_j = b x^j (j < 8), C_k = sum_j a_{8k+j} B_j, a b = C_0 ^ x^8 (C_1 ^ x^8 (C_2
-// ^ x^8 C_3)), and v x^8 = T0[v & 255] ^ v >> 8 -- one LDS lookup (slice
-// table 0's replica) per byte instead of eight shift-reduce steps.  Bit
-// 31 - i of a is its x^i coefficient (reflected).
-__device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* lsl, const LaneBase& lb, uint32_t a, uint32_t b) {
-  uint32_t B[8];
-  B[0] = b;
-#pragma unroll
-  for (int j = 1; j < 8; ++j)
-    B[j] = (B[j - 1] >> 1) ^ ((uint32_t)__builtin_amdgcn_sbfe((int)B[j - 1], 0, 1) & kPolyReflected);
-  const uint8_t* sl = lsl + kSliceOff;
-  uint32_t p = 0u;
-#pragma unroll
-  for (int k = 3; k >= 0; --k) {
-    if (k < 3) p = lds_u32(sl, __builtin_amdgcn_perm(p, lb.t0, 0x0C020400u)) ^ (p >> 8);  // p x^8
-#pragma unroll
-    for (int j = 0; j < 8; ++j) p ^= (uint32_t)__builtin_amdgcn_sbfe((int)a, 31 - (8 * k + j), 1) & B[j];
-  }
-  return p;
-}
-
 // shift(v, 4096 d) for d = 1..4 from the fold's byte-sliced tables (tab =
 // (d - 1) * 4096, per lane): one level of four lookups (one copy: bank
 // conflicts, but half the fold's LDS reads and a quarter of its VALU of the
@@ -408,50 +418,48 @@ __device__ __forceinline__ bool fold_out(const RegionGeom& g, const uint8_t* lds
   const uint64_t s = f.s, e = f.s + f.L;
   const uint64_t c0 = s >> 12, c1 = (e - 1u) >> 12;
   const uint32_t os = (uint32_t)(s & (kChunk - 1u)), oe = (uint32_t)(e - (c1 << 12));  // oe in [1, 4096]
-  const uint32_t r0 = g.raws[c0], r1 = g.raws[c1], rm = g.raws[min(c0 + 1u, c1)];
+  const uint32_t r0 = g.raws[c0], r1 = g.raws[c1];
   if ((os && (q_s.z != g.gen || q_s.w != ti)) || (oe != kChunk && (q_e.z != g.gen || q_e.w != ti))) return false;
   const uint32_t qs = os ? q_s.x : 0u;                                   // chunk c0's bytes before s, at its end
   const uint32_t T = (os ? quad_prefix_lds(lsl, lb, q_s.y, f.vs, s & 63u) : 0u) ^ f.ninit;  // R(s) ^ ~init, at s
   const uint32_t ze = oe == kChunk ? r1 : q_e.x;                         // chunk c1's bytes before e, at its end
   const uint32_t re = oe == kChunk ? 0u : quad_prefix_lds(lsl, lb, q_e.y, f.ve, e & 63u);  // R(e), at e
-  if (c1 <= c0 + 1u) {
-    // one or two chunks, one formula (a slice holding both kinds would run
-    // both branches): the data terms at chunk c1's end -- Qe(s) (one chunk)
-    // or shift4096(Qe(s) ^ raw c0) (two) -- ^ Ze, unshifted to e, and T
-    // straight to e:  (X ^ Ze) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e)
-    // (for two chunks x^(-8(4096 - oe)) x^(8(8192 - os)) = x^(8L))
-    const uint32_t sh = shc_lds(lds, qs ^ r0, 0u);
-    v = gf_mul_lds(lsl, lb, f.xe, (c1 == c0 ? qs : sh) ^ ze) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ re;
-    return true;
-  }
-  // Longer: Ze'(s) = Qe(s) ^ T x^(8(4096 - os)) at chunk c0's end, then up
-  // to four chunks per step -- acc at chunk c + k's end = shift(acc, 4096 k)
-  // ^ the raws of chunks c + 1 .. c + k below c1, each shifted by its own
-  // distance (independent of acc: one dependent lookup level per step) --,
-  // unshifted from c1's end.  The next step's raws are in flight meanwhile.
-  (void)rm;
-  uint32_t acc = qs ^ gf_mul_lds(lsl, lb, f.xs, T) ^ r0;
-  uint32_t rr[4];
+  // One formula for every length: the data terms at chunk c1's end -- X =
+  // Qe(s) (one chunk), shift4096(Qe(s) ^ raw c0) (two), or that chained
+  // over the chunks in between (longer) -- ^ Ze, unshifted to e, and T
+  // straight to e:  (X ^ Ze) x^(-8(4096 - oe)) ^ T x^(8L) ^ R(e)
+  // (x^(8L) from fold_in, so T stays off the chain; one- and two-chunk
+  // buffers in one slice run no branch of their own).
+  uint32_t X = c1 == c0 ? qs : shc_lds(lds, qs ^ r0, 0u);
+  if (c1 > c0 + 1u) {
+    // longer: from chunk c0's end up to four chunks per step -- acc at
+    // chunk c + k's end = shift(acc, 4096 k) ^ the raws of chunks c + 1 ..
+    // c + k below c1, each shifted by its own distance (independent of acc:
+    // one dependent lookup level per step); the next step's raws in flight
+    uint32_t acc = qs ^ r0;
+    uint32_t rr[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) rr[j] = g.raws[min(c0 + 1u + (uint64_t)j, c1 - 1u)];
-  for (uint64_t c = c0; c < c1;) {
-    const uint32_t k = (uint32_t)min(c1 - c, (uint64_t)4);
-    const uint64_t cn = c + k;
-    uint32_t rn[4];
+    for (int j = 0; j < 4; ++j) rr[j] = g.raws[min(c0 + 1u + (uint64_t)j, c1 - 1u)];
+    for (uint64_t c = c0; c < c1;) {
+      const uint32_t k = (uint32_t)min(c1 - c, (uint64_t)4);
+      const uint64_t cn = c + k;
+      uint32_t rn[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) rn[j] = g.raws[min(cn + 1u + (uint64_t)j, c1 - 1u)];
-    uint32_t x = shc_lds(lds, acc, (k - 1u) << 12);
+      for (int j = 0; j < 4; ++j) rn[j] = g.raws[min(cn + 1u + (uint64_t)j, c1 - 1u)];
+      uint32_t x = shc_lds(lds, acc, (k - 1u) << 12);
 #pragma unroll
-    for (uint32_t j = 1; j <= 4u; ++j) {  // chunk c + j: below c1 iff c + j < c1 (then j <= k)
-      const uint32_t rj = c + j < c1 ? rr[j - 1u] : 0u;
-      x ^= j < k ? shc_lds(lds, rj, (k - j - 1u) << 12) : rj;  // (j > k: rj = 0)
+      for (uint32_t j = 1; j <= 4u; ++j) {  // chunk c + j: below c1 iff c + j < c1 (then j <= k)
+        const uint32_t rj = c + j < c1 ? rr[j - 1u] : 0u;
+        x ^= j < k ? shc_lds(lds, rj, (k - j - 1u) << 12) : rj;  // (j > k: rj = 0)
+      }
+      acc = x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rr[j] = rn[j];
+      c = cn;
     }
-    acc = x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) rr[j] = rn[j];
-    c = cn;
+    X = acc;
   }
-  v = gf_mul_lds(lsl, lb, f.xe, acc ^ ze) ^ re;
+  v = gf_mul_lds(lsl, lb, f.xe, X ^ ze) ^ gf_mul_lds(lsl, lb, f.xt, T) ^ re;
   return true;
 }
 
@@ -710,16 +718,16 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return (uint64_t)cs + 4u * (uint64_t)uniform_u32(v);
   };
+  const uint8_t* lsl = lds + (kRSliceOff - kSliceOff);
   uint64_t k = claim();
   FoldIn f;
-  if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
+  if (k < nsl) f = fold_in(g, ka.tables, lsl, lb, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
   const uint4 shc = reinterpret_cast<const uint4*>(ka.tables + kTabShc)[threadIdx.x];  // 16 KiB: one per thread
   static_assert(kTabShc % 4u == 0 && 4u * 1024u == 4u * (uint32_t)kThreads, "fold tables: one uint4 per thread");
   __syncthreads();  // every unit done: the nibble tables are free
   reinterpret_cast<uint4*>(lds + kRShcOff)[threadIdx.x] = shc;
   __syncthreads();
   NVL_TL(3);
-  const uint8_t* lsl = lds + (kRSliceOff - kSliceOff);
   uint32_t adopt = 0u;  // empty SIMDs whose slices this wave takes over
   {
     const uint32_t wc = *region_slot(lds, kSlotWaves);
@@ -741,13 +749,13 @@ __device__ __forceinline__ void run_region(const RegionGeom& g, const KArgs& ka,
         ka.out[i] = finish(~v, ka.flags);
       }
       k = claim();
-      if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
+      if (k < nsl) f = fold_in(g, ka.tables, lsl, lb, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
     }
     if (!adopt) break;
     cs = (uint32_t)__builtin_ctz(adopt);
     adopt &= adopt - 1u;
     k = claim();
-    if (k < nsl) f = fold_in(g, ka.tables, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
+    if (k < nsl) f = fold_in(g, ka.tables, lsl, lb, min(ib + 64u * k + (uint64_t)lane, ib1 - 1u), c0w, B1);
   }
   NVL_TL_END();
 }

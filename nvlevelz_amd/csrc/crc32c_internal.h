@@ -25,11 +25,13 @@ namespace nvl {
 //                                     verbatim into LDS)
 //   [28740,32836) shc[4][4][256]     shift by 4096 d bytes (d = 1..4), byte-sliced (region fold: copied
 //                                     into LDS over the nibble tables' upper half once the chunks are done)
+//   [32836,33092) pw4k[256]          x^(8*4096*q) mod P, q = 0..255  (region fold: x^(8L) of a long buffer)
 constexpr uint32_t kXp8Len = 8193;  // a buffer spanning at most two chunks has at most 8192 bytes
 constexpr uint32_t kTabXp8 = 8256, kTabXm8 = kTabXp8 + kXp8Len;
 constexpr uint32_t kTabNib = (kTabXm8 + 4096u + 3u) & ~3u;
 constexpr uint32_t kTabShc = kTabNib + 8u * 16u * 64u;
-constexpr uint32_t kTableWords = kTabShc + 4u * 1024u;
+constexpr uint32_t kTabPw4k = kTabShc + 4u * 1024u;
+constexpr uint32_t kTableWords = kTabPw4k + 256u;
 
 // A portion of one buffer processed inside one work unit (fix-up input).
 struct Rec {

@@ -527,11 +527,11 @@ SHC = [shift_op(4096 * d) for d in (1, 2, 3, 4)]  # the fold's chunk shifts (blo
 
 def region_fold_steps(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     """The region kernel's fold of a buffer over three or more chunks
-    (fold_out's long branch): Ze'(s) at chunk c0's end, then up to four
-    chunks per step -- acc at chunk c + k's end = shift(acc, 4096 k) ^ the
-    raws of chunks c + 1 .. c + k below c1, each shifted by its distance to
-    c + k -- and unshifted from c1's end; the same value as region_fold's
-    chunk-by-chunk chain."""
+    (fold_out): X = Qe(s) ^ raw c0 at chunk c0's end, then up to four chunks
+    per step -- acc at chunk c + k's end = shift(acc, 4096 k) ^ the raws of
+    chunks c + 1 .. c + k below c1, each shifted by its distance to c + k --
+    unshifted from c1's end, and T = R(s) ^ ~init moved straight to e by
+    x^(8L); the same value as region_fold's chunk-by-chunk chain."""
     e = s + L
     c0, os_ = s >> 12, s & 4095
     c1, oe = (e - 1) >> 12, e - ((e - 1) >> 12 << 12)
@@ -539,7 +539,7 @@ def region_fold_steps(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
     ninit = (~init) & 0xFFFFFFFF
     qs = qe[("s", c0, os_)] if os_ else 0
     T = (piece_prefix_raw(mem, s) if os_ else 0) ^ ninit
-    acc = qs ^ shift(T, 4096 - os_) ^ raws[c0]
+    acc = qs ^ raws[c0]
     c = c0
     while c < c1:
         k = min(c1 - c, 4)
@@ -550,7 +550,7 @@ def region_fold_steps(mem: bytes, raws, qe, s: int, L: int, init: int) -> int:
         acc, c = x, c + k
     ze = raws[c1] if oe == 4096 else qe[("e", c1, oe)]
     re = 0 if oe == 4096 else piece_prefix_raw(mem, e)
-    v = unshift(acc ^ ze, 4096 - oe) ^ re
+    v = unshift(acc ^ ze, 4096 - oe) ^ shift(T, L) ^ re
     return (~v) & 0xFFFFFFFF
 
 

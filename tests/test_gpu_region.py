@@ -146,6 +146,28 @@ def test_region_tiny_and_mixed(dev, C, port):
     _check(C, dev, port, host, torch.from_numpy(host).to(dev), offs2, lens2, 12)
 
 
+@pytest.mark.parametrize("shaped", [False, True])
+def test_region_long_buffers(dev, C, port, shaped):
+    """Buffers of three chunks and more: the fold's chain of up to four
+    chunks per step (every remainder 1..4, chunk-aligned ends) and x^(8L)
+    for T -- from the tables up to 1 MiB, through x^(2^k) beyond (the
+    region kernel runs such buffers only under NVL_CRC32C_FLAG_REGION_SHAPED:
+    the checked entry routes buffers over 128 KiB to the batch kernels)."""
+    lens = [8193, 8192 + 4097, 4 * 4096, 5 * 4096 + 1, 6 * 4096 - 1, 7 * 4096, 9 * 4096 + 100, 65543, 131072,
+            (1 << 20) - 1, (1 << 20) + 5, 3 * (1 << 20) + 4097, 130000, 3, 4097, 64]
+    rng = np.random.default_rng(77)
+    gaps = rng.integers(0, 9, len(lens))
+    offs, host = _packed(port, lens, 0, 0x10E6, lead=5)
+    offs = offs + np.cumsum(gaps) - gaps
+    host = port.fill(0x10E6, 0, int(offs[-1] + lens[-1]) + 64)
+    buf = torch.from_numpy(host).to(dev)
+    inits = rng.integers(0, 2**32, size=len(lens), dtype=np.uint64).astype(np.uint32)
+    want = port.varlen(host, offs.astype(np.uint64), np.asarray(lens, dtype=np.uint64), inits)
+    it = torch.from_numpy(inits.view(np.int32)).to(dev)
+    got = _u32(C.extend_region(buf, _t64(offs, dev), _t64(lens, dev), it, shaped=shaped))
+    assert np.array_equal(got, want), np.nonzero(got != want)[0]
+
+
 @pytest.mark.parametrize("skew", [1, 5, 2049])
 def test_region_unaligned_region_pointer(dev, C, port, skew):
     """The region tensor starts `skew` bytes into an allocation: the chunk

@@ -83,6 +83,7 @@ constexpr uint64_t kTailWin = 4096;       // last bytes of the file read first: 
 constexpr uint64_t kMetaMax = 64u << 10;  // metaindex (+ trailer) bytes the fast path reads
 constexpr uint64_t kIndexPiece = 4096;    // the index block is checked as pieces of this size (crc32c_table_dev.hip)
 constexpr uint64_t kResHead = 32;         // device results: u32 bad, pad, u64 n_bad, u64 n_fix, pad
+constexpr uint64_t kRecSideMin = 4096;    // more data blocks: their records come back on the side stream
 constexpr uint8_t kCompute = 0xFF;
 
 // CRC32C(A || B) = shift(CRC32C(A), |B|) ^ CRC32C(B): the index block's
@@ -107,12 +108,19 @@ struct PieceFold {
 // *done = false: the caller runs the generic core (nothing written here is
 // kept).  On *done = true the result is final.
 //
-// Streams: on `st` the metaindex copy, the index parse (data slots and
-// records), the batch over data blocks + index pieces + meta blocks, the
-// trailer checks and the results copy; on the thread's side stream, once the
-// parse is done, the records copy into the caller's array -- it overlaps the
-// batch.  Records carry the verdict OK for every checked block; only when a
-// check fails (n_fix > 0) are the verdicts copied and patched in.
+// One host round trip before the batch -- the file's tail: the footer, the
+// index block's tail and, for a table without filter blocks (a few-byte
+// metaindex right before the index), the metaindex -- then everything on the
+// streams at once: on `st` the index parse (data slots, records, the meta
+// blocks' places as zero-length fillers, the index pieces), ONE region batch
+// in file order, the trailer checks and the results copy; on the thread's
+// side stream, once the parse is done, the records copy.  A metaindex outside
+// the tail is copied first on `st` and parsed on the host while the batch
+// runs, and meta blocks (filter blocks) get a batch of their own after the
+// main one.  Results and records land in pinned memory (a copy into the
+// caller's pageable array waits for the stream inside the copy call).
+// Records carry the verdict OK for every checked block; only when a check
+// fails (n_fix > 0) are the verdicts copied and patched in.
 int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t cap, size_t* n_blocks,
                uint32_t* table_status, uint64_t* n_bad, hipStream_t st, bool* done) {
   *done = false;
@@ -124,8 +132,8 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   if (!thread_table_aux(dev, &side, &ev_meta, &ev_parse)) return NVL_CRC32C_EHIP;
   uint8_t* pin = static_cast<uint8_t*>(thread_table_pinned(kTailWin));
   if (!pin) return NVL_CRC32C_EHIP;
-  // 1. the file's last bytes: the footer, and the index block's tail when
-  //    the index ends there (TableBuilder writes it last, table_builder.cc:241-266)
+  // 1. the file's last bytes (TableBuilder writes the metaindex, the index
+  //    and the footer last, table_builder.cc:241-266)
   const uint64_t w = len < kTailWin ? len : kTailWin, w0 = len - w;
   if (hipMemcpyAsync(pin, f + w0, w, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
@@ -138,7 +146,11 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
       !block_in_file(index_h, len) || index_h.size < 4)
     return NVL_CRC32C_OK;
   const bool meta_in = block_in_file(meta_h, len);
-  if (meta_in && meta_h.size + NVL_BLOCK_TRAILER_SIZE > kMetaMax) return NVL_CRC32C_OK;
+  const uint64_t meta_bytes = meta_in ? meta_h.size + NVL_BLOCK_TRAILER_SIZE : 0;
+  if (meta_bytes > kMetaMax) return NVL_CRC32C_OK;
+  std::vector<uint8_t> meta_img;  // the metaindex when it came with the tail
+  if (meta_in && meta_h.offset >= w0) meta_img.assign(pin + (meta_h.offset - w0), pin + (meta_h.offset - w0) + meta_bytes);
+  const bool meta_copy = meta_in && meta_img.empty();  // (else copied on the stream below)
   // the index tail: num_restarts (its last 4 bytes), type byte, masked CRC
   const uint64_t tail_off = index_h.offset + index_h.size - 4;
   uint8_t tail[9];
@@ -159,88 +171,55 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   const uint64_t nm_max = meta_in ? meta_h.size / 3 + 1 : 0;  // entries take >= 3 bytes
   if (2 + nr > cap) return NVL_CRC32C_OK;                     // the generic walk reports ENOSPC
 
-  // 2. device workspace: [results][boff][blen][crc][vk][records][batch workspace]
-  //    Slots in file order: data [0, nr), meta + zero-length fillers [nr, pb),
-  //    index pieces [pb, pb + np): one region batch over the image.
+  // 2. device workspace: [results][records][boff][blen][crc][vk][region
+  //    workspace] [meta batch: off | len1, crc, verdicts, workspace].  Slots in
+  //    file order: data [0, nr), zero-length fillers at the index block's
+  //    offset [nr, pb) (the meta blocks' places), index pieces [pb, pb + np).
   const uint64_t pb = nr + nm_max, nmax = pb + np;
   if (nmax > 0xFFFFFFFFull) return NVL_CRC32C_OK;
-  const size_t s_res = up256(kResHead + 4 * np + nm_max), s8 = up256(nmax * 8), s4 = up256(nmax * 4),
-               s1 = up256(nmax), s_rec = up256(nr * sizeof(nvl_table_block));
+  const size_t s_res = up256(kResHead + 4 * np), s8 = up256(nmax * 8), s4 = up256(nmax * 4), s1 = up256(nmax),
+               s_rec = up256(nr * sizeof(nvl_table_block));
   const size_t wsb = nvl_crc32c_region_workspace_bytes(len, nmax);
-  uint8_t* d = static_cast<uint8_t*>(thread_table_device(dev, s_res + 2 * s8 + s4 + s1 + s_rec + wsb));
+  const size_t s_main = s_res + 2 * s8 + s4 + s1 + s_rec + up256(wsb);
+  const size_t m16 = up256(nm_max * 16), m4 = up256(nm_max * 4), m1 = up256(nm_max);
+  const size_t mwsb = nm_max ? nvl_crc32c_batch_workspace_bytes(nm_max) : 0;
+  uint8_t* d = static_cast<uint8_t*>(thread_table_device(dev, s_main + m16 + m4 + m1 + mwsb));
   if (!d) return NVL_CRC32C_EHIP;
   uint8_t* dres = d;
-  uint64_t* boff = reinterpret_cast<uint64_t*>(d + s_res);
-  uint64_t* blen = reinterpret_cast<uint64_t*>(d + s_res + s8);
-  uint32_t* crc = reinterpret_cast<uint32_t*>(d + s_res + 2 * s8);
-  uint8_t* vk = d + s_res + 2 * s8 + s4;
-  nvl_table_block* rec = reinterpret_cast<nvl_table_block*>(d + s_res + 2 * s8 + s4 + s1);
-  void* ws = d + s_res + 2 * s8 + s4 + s1 + s_rec;
-  // pinned: [metaindex][meta + filler slots: off, len1 | vk][results]
-  const size_t p_meta = 0, p_slots = up256(kMetaMax), p_res = p_slots + up256(nm_max * 17);
-  pin = static_cast<uint8_t*>(thread_table_pinned(p_res + s_res));
+  nvl_table_block* rec = reinterpret_cast<nvl_table_block*>(d + s_res);  // (right after: one copy back for both)
+  uint64_t* boff = reinterpret_cast<uint64_t*>(d + s_res + s_rec);
+  uint64_t* blen = reinterpret_cast<uint64_t*>(d + s_res + s_rec + s8);
+  uint32_t* crc = reinterpret_cast<uint32_t*>(d + s_res + s_rec + 2 * s8);
+  uint8_t* vk = d + s_res + s_rec + 2 * s8 + s4;
+  void* ws = d + s_res + s_rec + 2 * s8 + s4 + s1;
+  uint64_t* moff = reinterpret_cast<uint64_t*>(d + s_main);  // [nm_max offsets][nm_max len1]
+  uint32_t* mcrc = reinterpret_cast<uint32_t*>(d + s_main + m16);
+  uint8_t* mver = d + s_main + m16 + m4;
+  void* mws = d + s_main + m16 + m4 + m1;
+  // pinned: [metaindex][meta slots: off | len1][meta verdicts][results][records]
+  const size_t p_meta = 0, p_slots = up256(kMetaMax), p_mver = p_slots + m16, p_res = p_mver + m1,
+               p_rec = p_res + s_res;
+  pin = static_cast<uint8_t*>(thread_table_pinned(p_rec + s_rec));
   if (!pin) return NVL_CRC32C_EHIP;
 
-  // 3. on st: the metaindex copy, then the index parse; the host waits for
-  //    the copy only
+  // 3. everything on the streams
   if (hipMemsetAsync(dres, 0, kResHead, st) != hipSuccess) return NVL_CRC32C_EHIP;
-  if (meta_in && hipMemcpyAsync(pin + p_meta, f + meta_h.offset, meta_h.size + NVL_BLOCK_TRAILER_SIZE,
-                                hipMemcpyDeviceToHost, st) != hipSuccess)
+  if (meta_copy &&
+      hipMemcpyAsync(pin + p_meta, f + meta_h.offset, meta_bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
     return NVL_CRC32C_EHIP;
-  if (hipEventRecord(ev_meta, st) != hipSuccess ||
+  // The records (24 B per data block) come back with the results after the
+  // batch -- or, for a large index, on the side stream once the parse has
+  // written them, overlapping the batch (10^5 blocks: 2.4 MB).
+  const bool rec_side = nr > kRecSideMin;
+  if ((meta_copy && hipEventRecord(ev_meta, st) != hipSuccess) ||
       launch_index_entries(f, len, index_h.offset, index_h.size, (uint32_t)nr, (uint32_t)np, (uint32_t)pb, boff, blen,
                            vk, rec, reinterpret_cast<uint32_t*>(dres), st) != hipSuccess ||
-      hipEventRecord(ev_parse, st) != hipSuccess || hipEventSynchronize(ev_meta) != hipSuccess)
+      (rec_side && hipEventRecord(ev_parse, st) != hipSuccess))
     return NVL_CRC32C_EHIP;
-  uint8_t v_meta = NVL_BLOCK_TRUNCATED;
-  std::vector<nvl_block_handle> meta_blocks;
-  std::vector<uint8_t> meta_bad;
-  if (meta_in) {
-    const uint8_t* mb = pin + p_meta;
-    v_meta = host_block_verdict(mb, meta_h.size);
-    if (v_meta == NVL_BLOCK_OK && mb[meta_h.size] == 0) block_handles(mb, meta_h.size, &meta_blocks, &meta_bad);
-  }
-  const uint64_t nm = meta_blocks.size(), n = nmax, cnt = 2 + nm + nr;
-  if (nm > nm_max || cnt > cap) {  // (nm_max bounds it) / the generic walk reports ENOSPC
+  auto drain = [&]() {  // (the workspace and the pinned buffers are the thread's: nothing may still use them)
     (void)hipStreamSynchronize(st);
-    return NVL_CRC32C_OK;
-  }
-
-  // 4. meta slots and fillers [nr, pb), then ONE region batch over data
-  //    blocks + meta blocks + index pieces.  A zero-length filler sits at the
-  //    index block's offset (between the meta blocks and the first piece, so
-  //    the slots stay in file order); a meta slot that is not read gets length
-  //    0 at the previous slot's end for the same reason.
-  const uint64_t nf = nm_max;
-  uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
-  uint8_t* mv = pin + p_slots + nf * 16;
-  // (a leading slot that is not read sits at the first read meta block's
-  // offset, else at the index block's: never before the data blocks)
-  uint64_t prev_end = index_h.offset;
-  for (uint64_t j = 0; j < nm; ++j) {
-    if (!meta_bad[j] && block_in_file(meta_blocks[j], len)) {
-      prev_end = meta_blocks[j].offset;
-      break;
-    }
-  }
-  for (uint64_t j = 0; j < nf; ++j) {
-    if (j < nm) {
-      const nvl_block_handle& b = meta_blocks[j];
-      const bool fits = !meta_bad[j] && block_in_file(b, len);
-      ms[j] = fits ? b.offset : prev_end;
-      ms[nf + j] = fits ? b.size + 1 : 0;
-      mv[j] = meta_bad[j] ? (uint8_t)NVL_BLOCK_BAD_HANDLE : (fits ? kCompute : (uint8_t)NVL_BLOCK_TRUNCATED);
-      if (fits) prev_end = b.offset + b.size + 1;
-    } else {
-      ms[j] = index_h.offset;
-      ms[nf + j] = 0;
-      mv[j] = (uint8_t)NVL_BLOCK_OK;  // no verdict of its own
-    }
-  }
-  if (nf && (hipMemcpyAsync(boff + nr, ms, nf * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-             hipMemcpyAsync(blen + nr, ms + nf, nf * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-             hipMemcpyAsync(vk + nr, mv, nf, hipMemcpyHostToDevice, st) != hipSuccess))
-    return NVL_CRC32C_EHIP;
+    if (rec_side) (void)hipStreamSynchronize(side);
+  };
   // Up to kShapedMaxSlots slots, one launch (NVL_CRC32C_FLAG_REGION_SHAPED):
   // a table's slots are in file order by construction (table/table_builder.cc
   // writes data blocks, meta blocks, the metaindex and the index in sequence,
@@ -253,23 +232,68 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   // so larger tables keep the checked entry, whose plan sends such a batch to
   // the batch kernels (tests/test_table_verify.py::test_table_dev_out_of_order_index).
   constexpr uint64_t kShapedMaxSlots = 8192;
-  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, n,
-                                 n <= kShapedMaxSlots ? NVL_CRC32C_FLAG_REGION_SHAPED : 0u, ws, wsb, st);
+  int rc = nvl_crc32c_region_dev(f, len, boff, blen, nullptr, 0, crc, nmax,
+                                 nmax <= kShapedMaxSlots ? NVL_CRC32C_FLAG_REGION_SHAPED : 0u, ws, wsb, st);
+  if (rc == NVL_CRC32C_OK &&
+      (launch_table_verdicts(f, boff, blen, crc, nmax, (uint32_t)nr, 0u, (uint32_t)pb, (uint32_t)np, vk, dres, st) !=
+           hipSuccess ||
+       hipMemcpyAsync(pin + p_res, dres, rec_side ? kResHead + 4 * np : s_res + nr * sizeof(nvl_table_block),
+                      hipMemcpyDeviceToHost, st) != hipSuccess ||
+       (rec_side && (hipStreamWaitEvent(side, ev_parse, 0) != hipSuccess ||
+                     hipMemcpyAsync(pin + p_rec, rec, nr * sizeof(nvl_table_block), hipMemcpyDeviceToHost, side) !=
+                         hipSuccess))))
+    rc = NVL_CRC32C_EHIP;
+  if (rc != NVL_CRC32C_OK) {
+    drain();
+    return rc;
+  }
+
+  // 4. the metaindex on the host while the batch runs, then its meta blocks'
+  //    own batch and trailer checks after the main one
+  if (meta_copy && hipEventSynchronize(ev_meta) != hipSuccess) {
+    drain();
+    return NVL_CRC32C_EHIP;
+  }
+  uint8_t v_meta = NVL_BLOCK_TRUNCATED;
+  std::vector<nvl_block_handle> meta_blocks;
+  std::vector<uint8_t> meta_bad;
+  if (meta_in) {
+    const uint8_t* mb = meta_copy ? pin + p_meta : meta_img.data();
+    v_meta = host_block_verdict(mb, meta_h.size);
+    if (v_meta == NVL_BLOCK_OK && mb[meta_h.size] == 0) block_handles(mb, meta_h.size, &meta_blocks, &meta_bad);
+  }
+  const uint64_t nm = meta_blocks.size(), cnt = 2 + nm + nr;
+  if (nm > nm_max || cnt > cap) {  // (nm_max bounds it) / the generic walk reports ENOSPC
+    drain();
+    return NVL_CRC32C_OK;
+  }
+  std::vector<uint8_t> mv(nm);  // the meta blocks' verdicts (kCompute: from the meta batch, in order)
+  uint64_t nq = 0;
+  uint64_t* ms = reinterpret_cast<uint64_t*>(pin + p_slots);
+  for (uint64_t j = 0; j < nm; ++j) {
+    const nvl_block_handle& b = meta_blocks[j];
+    mv[j] = meta_bad[j] ? (uint8_t)NVL_BLOCK_BAD_HANDLE
+                        : (block_in_file(b, len) ? kCompute : (uint8_t)NVL_BLOCK_TRUNCATED);
+    if (mv[j] == kCompute) {
+      ms[nq] = b.offset;
+      ms[nm_max + nq] = b.size + 1;
+      ++nq;
+    }
+  }
+  if (nq) {
+    if (hipMemcpyAsync(moff, ms, nm_max * 16, hipMemcpyHostToDevice, st) != hipSuccess) rc = NVL_CRC32C_EHIP;
+    if (rc == NVL_CRC32C_OK) rc = nvl_crc32c_batch_dev(f, moff, moff + nm_max, nullptr, 0, mcrc, nq, 0, mws, mwsb, st);
+    if (rc == NVL_CRC32C_OK &&
+        (launch_trailer_verdicts(f, moff, moff + nm_max, mcrc, nq, mver, st) != hipSuccess ||
+         hipMemcpyAsync(pin + p_mver, mver, nq, hipMemcpyDeviceToHost, st) != hipSuccess))
+      rc = NVL_CRC32C_EHIP;
+  }
+  const hipError_t e1 = hipStreamSynchronize(st), e2 = rec_side ? hipStreamSynchronize(side) : hipSuccess;
   if (rc != NVL_CRC32C_OK) return rc;
-  const size_t res_bytes = kResHead + 4 * np + nm;
-  uint8_t* res = pin + p_res;
-  if (launch_table_verdicts(f, boff, blen, crc, n, (uint32_t)nr, (uint32_t)nm, (uint32_t)pb, (uint32_t)np, vk,
-                            dres, st) != hipSuccess ||
-      hipMemcpyAsync(res, dres, res_bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
-    return NVL_CRC32C_EHIP;
-  // the records, on the side stream once the parse has written them
-  if (hipStreamWaitEvent(side, ev_parse, 0) != hipSuccess ||
-      hipMemcpyAsync(blocks + 2 + nm, rec, nr * sizeof(nvl_table_block), hipMemcpyDeviceToHost, side) != hipSuccess)
-    return NVL_CRC32C_EHIP;
-  const hipError_t e1 = hipStreamSynchronize(st), e2 = hipStreamSynchronize(side);
   if (e1 != hipSuccess || e2 != hipSuccess) return NVL_CRC32C_EHIP;
 
   // 5. the index block's own check (Table::Open, table.cc:58-66) from its pieces
+  const uint8_t* res = pin + p_res;
   uint32_t bad;
   uint64_t nb, nfix;
   memcpy(&bad, res, 4);
@@ -279,6 +303,7 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   const uint32_t* pc = reinterpret_cast<const uint32_t*>(res + kResHead);
   const bool index_ok = pf.fold(pc, np, ilen) == unmask(le32(tail + 5));
   if (bad || !index_ok) return NVL_CRC32C_OK;  // not the walk's list, or the index fails: generic
+  memcpy(blocks + 2 + nm, pin + p_rec, nr * sizeof(nvl_table_block));
   if (nfix) {  // some data block failed its check: its verdict replaces the record's OK
     std::vector<uint8_t> v(nr);
     if (hipMemcpyAsync(v.data(), vk, nr, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -288,12 +313,15 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   }
   blocks[0] = nvl_table_block{index_h.offset, index_h.size, NVL_TBLOCK_INDEX, NVL_BLOCK_OK};
   blocks[1] = nvl_table_block{meta_h.offset, meta_h.size, NVL_TBLOCK_METAINDEX, v_meta};
-  const uint8_t* mvr = res + kResHead + 4 * np;
-  for (uint64_t j = 0; j < nm; ++j)
-    blocks[2 + j] = nvl_table_block{meta_blocks[j].offset, meta_blocks[j].size, NVL_TBLOCK_META, mvr[j]};
+  uint64_t meta_not_ok = 0;
+  for (uint64_t j = 0, q = 0; j < nm; ++j) {
+    const uint8_t v = mv[j] == kCompute ? pin[p_mver + q++] : mv[j];
+    blocks[2 + j] = nvl_table_block{meta_blocks[j].offset, meta_blocks[j].size, NVL_TBLOCK_META, v};
+    meta_not_ok += v != NVL_BLOCK_OK;
+  }
   *n_blocks = cnt;
   *table_status = NVL_TABLE_OK;
-  if (n_bad) *n_bad = nb + (v_meta != NVL_BLOCK_OK);
+  if (n_bad) *n_bad = nb + meta_not_ok + (v_meta != NVL_BLOCK_OK);
   *done = true;
   return NVL_CRC32C_OK;
 }

@@ -58,22 +58,30 @@ constexpr uint64_t kResHead = 32;    // res: u32 bad, pad, u64 n_bad, u64 n_fix,
 // Batch slots, in file order (TableBuilder writes data blocks, meta blocks,
 // the metaindex, the index: table_builder.cc:241-266) so that the batch runs
 // as one region (nvl_crc32c_region_dev): [0, nr) the data blocks the index
-// entries point at, [nr, pb) the meta blocks and zero-length fillers (the
-// host writes those), [pb, pb + np) the index block itself in np pieces of
-// 4096 bytes (the last one shorter; their CRCs are combined on the host).
+// entries point at, [nr, pb) zero-length fillers at the index block's offset
+// (the meta blocks' places: they get a batch of their own), [pb, pb + np) the
+// index block itself in np pieces of 4096 bytes (the last one shorter; their
+// CRCs are combined on the host).
 // Thread i < nr parses entry i of the index block [blk, blk + size) with nr
 // restart points -> slot i (offset, size + 1: block | type; length 0 with a
 // verdict preset when the handle is bad or out of the file) and output record
 // rec[i] = {offset, size, NVL_TBLOCK_DATA, preset or OK}; *bad |= 1 when the
 // entry is not where the sequential walk would find it.  Thread nr + k writes
-// piece slot pb + k.
+// piece slot pb + k, thread nr + np + j filler slot nr + j.
 __global__ void crc32c_index_entries(const uint8_t* __restrict__ file, uint64_t file_len, uint64_t index_off,
                                      uint64_t size, uint32_t nr, uint32_t np, uint32_t pb,
                                      uint64_t* __restrict__ boff, uint64_t* __restrict__ blen,
                                      uint8_t* __restrict__ vk, nvl_table_block* __restrict__ rec,
                                      uint32_t* __restrict__ bad) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (uint64_t)nr + np) return;
+  if (t >= (uint64_t)pb + np) return;
+  if (t >= (uint64_t)nr + np) {  // a filler: nothing to read, no verdict of its own
+    const uint64_t i = t - np;
+    boff[i] = index_off;
+    blen[i] = 0;
+    vk[i] = (uint8_t)NVL_BLOCK_OK;
+    return;
+  }
   if (t >= nr) {
     const uint64_t k = t - nr, o = k * kPiece, ilen = size + 1, i = pb + k;
     boff[i] = index_off + o;
@@ -161,7 +169,7 @@ __global__ void crc32c_table_verdicts(const uint8_t* __restrict__ file, const ui
 hipError_t launch_index_entries(const void* file, uint64_t file_len, uint64_t index_off, uint64_t size, uint32_t nr,
                                 uint32_t np, uint32_t pb, uint64_t* boff, uint64_t* blen, uint8_t* vk,
                                 nvl_table_block* rec, uint32_t* bad, hipStream_t st) {
-  const uint64_t threads = (uint64_t)nr + np;
+  const uint64_t threads = (uint64_t)pb + np;  // data entries, index pieces, fillers [nr, pb)
   if (threads == 0) return hipSuccess;
   hipLaunchKernelGGL(dev::crc32c_index_entries, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, st,
                      static_cast<const uint8_t*>(file), file_len, index_off, size, nr, np, pb, boff, blen, vk, rec,

@@ -1230,6 +1230,49 @@ int nvl_crc32c_fixed_dev_multi(const nvl_crc32c_shard* shards, int nshards, uint
   return rc;
 }
 
+// `st` (on dst_device, current) waits for the work enqueued so far on the
+// shard's stream, unless that is `st` itself.
+static hipError_t after_shard(const nvl_crc32c_shard& sh, int dst_device, hipStream_t st) {
+  hipStream_t ss = nullptr;
+  if (shard_stream(sh, &ss) != NVL_CRC32C_OK) return hipErrorInvalidValue;
+  if (ss == st && sh.device == dst_device) return hipSuccess;
+  hipError_t e;
+  hipEvent_t ev = nullptr;
+  if ((e = hipSetDevice(sh.device)) == hipSuccess &&
+      (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) == hipSuccess &&
+      (e = hipEventRecord(ev, ss)) == hipSuccess && (e = hipSetDevice(dst_device)) == hipSuccess)
+    e = hipStreamWaitEvent(st, ev, 0);
+  if (ev) (void)hipEventDestroy(ev);  // (released once the recorded work is done)
+  (void)hipSetDevice(dst_device);
+  return e;
+}
+
+// Whether kernels on `dev` may read memory of `peer` (peer access enabled
+// once per pair, process-wide; a pair that cannot gathers by peer copies).
+static bool peer_mapped(int dev, int peer) {
+  if (dev < 0 || peer < 0 || dev >= kMaxDevices || peer >= kMaxDevices) return false;
+  static std::atomic<int8_t> s_state[kMaxDevices][kMaxDevices];  // 0 unknown, 1 mapped, -1 not
+  std::atomic<int8_t>& s = s_state[dev][peer];
+  int8_t v = s.load(std::memory_order_acquire);
+  if (v) return v > 0;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((v = s.load(std::memory_order_relaxed))) return v > 0;
+  int can = 0;
+  bool ok = hipDeviceCanAccessPeer(&can, dev, peer) == hipSuccess && can;
+  if (ok) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+    if (cur >= 0) (void)hipSetDevice(cur);
+  }
+  (void)hipGetLastError();
+  s.store(ok ? 1 : -1, std::memory_order_release);
+  return ok;
+}
+
 int nvl_crc32c_gather_dev(uint32_t* dst, int dst_device, const nvl_crc32c_shard* shards, int nshards,
                           uint32_t layout, void* stream) {
   if (!dst || !shards || nshards <= 0 || nshards > 4096 || layout > NVL_CRC32C_GATHER_ROUND_ROBIN)
@@ -1253,6 +1296,34 @@ int nvl_crc32c_gather_dev(uint32_t* dst, int dst_device, const nvl_crc32c_shard*
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (hipSetDevice(dst_device) != hipSuccess) return NVL_CRC32C_ENODEV;
+  // One launch when every shard's results are on dst_device or peer-mapped
+  // to it (up to kGatherMax shards): the kernel reads each result where its
+  // shard wrote it (over xGMI for a peer) after the shards' streams.
+  bool direct = nshards <= (int)dev::kGatherMax;
+  for (int k = 0; k < nshards && direct; ++k)
+    if (shards[k].n && shards[k].device != dst_device) direct = peer_mapped(dst_device, shards[k].device);
+  if (direct) {
+    dev::GatherSrc gs{};
+    gs.G = (uint32_t)nshards;
+    gs.rr = layout == NVL_CRC32C_GATHER_ROUND_ROBIN ? 1u : 0u;
+    uint64_t pos = 0;
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < nshards && e == hipSuccess; ++k) {
+      const nvl_crc32c_shard& sh = shards[k];
+      gs.src[k] = sh.out;
+      gs.pos[k] = pos;
+      pos += sh.n;
+      if (sh.n) e = after_shard(sh, dst_device, st);
+    }
+    gs.pos[nshards] = pos;
+    if (e == hipSuccess) e = launch_gather(gs, N, dst, st);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return NVL_CRC32C_EHIP;
+    }
+    return NVL_CRC32C_OK;
+  }
   uint32_t* tmp = nullptr;
   const bool rr = layout == NVL_CRC32C_GATHER_ROUND_ROBIN && nshards > 1;
   hipError_t e = rr ? hipMallocAsync(reinterpret_cast<void**>(&tmp), std::max<uint64_t>(N, 1) * 4, st) : hipSuccess;
@@ -1263,20 +1334,7 @@ int nvl_crc32c_gather_dev(uint32_t* dst, int dst_device, const nvl_crc32c_shard*
     if (sh.n) {
       // after the shard's own stream (its results), then the copy: a peer
       // copy over xGMI for another device, a device copy for the same one
-      hipStream_t ss = nullptr;
-      if (shard_stream(sh, &ss) != NVL_CRC32C_OK) {
-        e = hipErrorInvalidValue;
-        break;
-      }
-      if (ss != st || sh.device != dst_device) {
-        hipEvent_t ev = nullptr;
-        if ((e = hipSetDevice(sh.device)) == hipSuccess &&
-            (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) == hipSuccess &&
-            (e = hipEventRecord(ev, ss)) == hipSuccess && (e = hipSetDevice(dst_device)) == hipSuccess)
-          e = hipStreamWaitEvent(st, ev, 0);
-        if (ev) (void)hipEventDestroy(ev);  // (released once the recorded work is done)
-        (void)hipSetDevice(dst_device);
-      }
+      e = after_shard(sh, dst_device, st);
       if (e == hipSuccess)
         e = sh.device == dst_device
                 ? hipMemcpyAsync(to + pos, sh.out, sh.n * 4, hipMemcpyDeviceToDevice, st)

@@ -127,6 +127,18 @@ hipError_t launch_region(const LaunchCtx& lc, const uint8_t* region, uint64_t re
                          const uint64_t* lengths, const uint32_t* init, uint32_t init_all, uint32_t* out, uint64_t n,
                          uint32_t flags, void* ws);
 
+// nvl_crc32c_gather_dev in one launch: up to kGatherMax shards' result arrays
+// on (or peer-mapped to) the destination device, round robin (rr) or
+// concatenated (shard k at [pos[k], pos[k+1])).
+namespace dev {
+constexpr uint32_t kGatherMax = 16;
+struct GatherSrc {
+  const uint32_t* src[kGatherMax];
+  uint64_t pos[kGatherMax + 1];
+  uint32_t G, rr;
+};
+}  // namespace dev
+hipError_t launch_gather(const dev::GatherSrc& s, uint64_t N, uint32_t* dst, hipStream_t st);
 // dst[i] = shard (i mod G)'s result (i div G) from the shards' results concatenated (nvl_crc32c_gather_dev)
 hipError_t launch_interleave_rr(const uint32_t* src, uint64_t N, uint32_t G, uint32_t* dst, hipStream_t st);
 hipError_t launch_read_probe(const void* src, uint64_t bytes, uint32_t* sink, hipStream_t st);

@@ -66,7 +66,34 @@ __global__ void interleave_rr_kernel(const uint32_t* __restrict__ src, uint64_t 
   }
 }
 
+// The gather in one launch (nvl_crc32c_gather_dev with at most kGatherMax
+// shards, every one on the destination device or peer-mapped to it): each
+// result read where its shard wrote it -- no staging copies, no interleave
+// pass.  rr: dst[i] = shard (i mod G)'s result (i div G); else shard k's
+// results at [pos[k], pos[k+1]).
+__global__ void gather_kernel(GatherSrc s, uint64_t N, uint32_t* __restrict__ dst) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t k = 0;
+    uint64_t j;
+    if (s.rr) {
+      k = (uint32_t)(i % s.G);
+      j = i / s.G;
+    } else {
+      while (k + 1u < s.G && i >= s.pos[k + 1]) ++k;
+      j = i - s.pos[k];
+    }
+    dst[i] = s.src[k][j];
+  }
+}
+
 }  // namespace dev
+
+hipError_t launch_gather(const dev::GatherSrc& s, uint64_t N, uint32_t* dst, hipStream_t st) {
+  if (N == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>((N + 255) / 256, 8192);
+  hipLaunchKernelGGL(dev::gather_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, s, N, dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_interleave_rr(const uint32_t* src, uint64_t N, uint32_t G, uint32_t* dst, hipStream_t st) {
   if (N == 0) return hipSuccess;

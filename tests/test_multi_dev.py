@@ -66,13 +66,14 @@ def dev():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G", [1, 2, 3, 8])
+@pytest.mark.parametrize("G", [1, 2, 3, 8, 16, 17])
 def test_round_robin_shards_reassemble_config5_order(dev, port, G):
     """N blocks of the config-5 stream split round-robin over G shards (shard
     k = global blocks k, k + G, ...: fill_splitmix's block_step), checksummed
     by fixed_dev_multi, gathered round-robin: the global CRC array equals the
     oracle's over the first N blocks, and the concatenated gather equals the
-    shards in order."""
+    shards in order.  (Up to 16 shards the gather is one kernel reading every
+    shard's results in place; 17 takes the copy-and-interleave path.)"""
     import torch
     N, B = 5003, 4096
     bufs, shards = [], []

@@ -340,7 +340,7 @@ __device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* lsl, const LaneBas
 __device__ uint32_t xpow8_long(const uint32_t* tables, const uint8_t* lsl, const LaneBase& lb, uint64_t L) {
   uint32_t p = gf_mul_lds(lsl, lb, tables[kTabXp8 + (L & (kChunk - 1u))], tables[kTabPw4k + ((L >> 12) & 255u)]);
   uint32_t b = 23;
-  for (uint64_t q = L >> 20; q; q >>= 1, ++b)
+  for (uint64_t q = L >> 20; q && b < 64u; q >>= 1, ++b)  // (x2n holds k < 64: L < 2^61)
     if (q & 1u) p = gf_mul_lds(lsl, lb, p, tables[kGX2n + b]);
   return p;
 }

@@ -221,10 +221,12 @@ NVL_API int nvl_crc32c_fixed_dev_multi(const nvl_crc32c_shard* shards, int nshar
                                        uint32_t flags);
 
 /* The shards' results gathered into ONE device array `dst` (on dst_device,
- * ordered on `stream`, a stream of dst_device or NULL for its null stream):
- * every shard's `out` is copied over xGMI (hipMemcpyPeerAsync,
- * 4 bytes per block: the only cross-device traffic) after that shard's
- * stream, then laid out by `layout`:
+ * ordered on `stream`, a stream of dst_device or NULL for its null stream),
+ * after each shard's stream: up to 16 shards on dst_device or peer-mapped to
+ * it (peer access is enabled once per device pair, process-wide) are read in
+ * place by one kernel -- over xGMI for a peer, 4 bytes per block: the only
+ * cross-device traffic; more shards, or a peer that cannot be mapped, are
+ * copied first (hipMemcpyPeerAsync) and then laid out.  Layouts:
  *   NVL_CRC32C_GATHER_CONCAT       shard 0's results, then shard 1's, ...
  *   NVL_CRC32C_GATHER_ROUND_ROBIN  global block i from shard i mod nshards
  *                                  (shard k must hold ceil((N - k) / nshards)

@@ -955,11 +955,11 @@ int nvl_crc32c_host_unregister(const void* ptr) {
   std::lock_guard<std::mutex> lk(g_reg_mu);
   auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
   if (!ptr || it == g_reg.end()) return NVL_CRC32C_EINVAL;
-  g_reg.erase(it);
-  if (hipHostUnregister(const_cast<void*>(ptr)) != hipSuccess) {
+  if (hipHostUnregister(const_cast<void*>(ptr)) != hipSuccess) {  // (still registered: the entry stays)
     (void)hipGetLastError();
     return NVL_CRC32C_EHIP;
   }
+  g_reg.erase(it);
   return NVL_CRC32C_OK;
 }
 

@@ -203,23 +203,27 @@ int table_fast(const uint8_t* f, uint64_t len, nvl_table_block* blocks, size_t c
   if (!pin) return NVL_CRC32C_EHIP;
 
   // 3. everything on the streams
-  if (hipMemsetAsync(dres, 0, kResHead, st) != hipSuccess) return NVL_CRC32C_EHIP;
-  if (meta_copy &&
-      hipMemcpyAsync(pin + p_meta, f + meta_h.offset, meta_bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
-    return NVL_CRC32C_EHIP;
-  // The records (24 B per data block) come back with the results after the
-  // batch -- or, for a large index, on the side stream once the parse has
-  // written them, overlapping the batch (10^5 blocks: 2.4 MB).
-  const bool rec_side = nr > kRecSideMin;
-  if ((meta_copy && hipEventRecord(ev_meta, st) != hipSuccess) ||
-      launch_index_entries(f, len, index_h.offset, index_h.size, (uint32_t)nr, (uint32_t)np, (uint32_t)pb, boff, blen,
-                           vk, rec, reinterpret_cast<uint32_t*>(dres), st) != hipSuccess ||
-      (rec_side && hipEventRecord(ev_parse, st) != hipSuccess))
-    return NVL_CRC32C_EHIP;
+  const bool rec_side = nr > kRecSideMin;  // (see below)
   auto drain = [&]() {  // (the workspace and the pinned buffers are the thread's: nothing may still use them)
     (void)hipStreamSynchronize(st);
     if (rec_side) (void)hipStreamSynchronize(side);
   };
+  if (hipMemsetAsync(dres, 0, kResHead, st) != hipSuccess ||
+      (meta_copy &&
+       hipMemcpyAsync(pin + p_meta, f + meta_h.offset, meta_bytes, hipMemcpyDeviceToHost, st) != hipSuccess)) {
+    drain();
+    return NVL_CRC32C_EHIP;
+  }
+  // The records (24 B per data block) come back with the results after the
+  // batch -- or, for a large index, on the side stream once the parse has
+  // written them, overlapping the batch (10^5 blocks: 2.4 MB).
+  if ((meta_copy && hipEventRecord(ev_meta, st) != hipSuccess) ||
+      launch_index_entries(f, len, index_h.offset, index_h.size, (uint32_t)nr, (uint32_t)np, (uint32_t)pb, boff, blen,
+                           vk, rec, reinterpret_cast<uint32_t*>(dres), st) != hipSuccess ||
+      (rec_side && hipEventRecord(ev_parse, st) != hipSuccess)) {
+    drain();
+    return NVL_CRC32C_EHIP;
+  }
   // Up to kShapedMaxSlots slots, one launch (NVL_CRC32C_FLAG_REGION_SHAPED):
   // a table's slots are in file order by construction (table/table_builder.cc
   // writes data blocks, meta blocks, the metaindex and the index in sequence,

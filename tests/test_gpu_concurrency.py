@@ -8,6 +8,7 @@ device-resident whole-table verify (the thread's table workspace, side
 stream, pinned buffers) and the host region entry from registered and
 unregistered memory (the thread's staging and result buffers).  Every result
 is checked against the oracle or against the same call made alone."""
+import os
 import threading
 
 import numpy as np
@@ -17,7 +18,9 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-THREADS, ITERS = 4, 5
+# (NVL_CONC_THREADS / NVL_CONC_ITERS widen it for a stress pass)
+THREADS = int(os.environ.get("NVL_CONC_THREADS", "4"))
+ITERS = int(os.environ.get("NVL_CONC_ITERS", "5"))
 
 
 @pytest.fixture(scope="module")
@@ -37,7 +40,6 @@ def _u32(t):
 
 def test_concurrent_entry_kinds(dev, port):
     import sys
-    import os
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     from nvlevelz_amd import crc32c, framing

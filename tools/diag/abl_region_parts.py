@@ -9,6 +9,7 @@ WRONG for every variant but `base` (NVL_CRC32C_SELFTEST_REPORT_ONLY=1).
   nofold      no fold phase at all (no barrier, no stores)
   noevents    nofold + no event records in the unit loop
   nowin       noevents + no metadata windows / searches (pure region streaming)
+  nostores    nofold + the event records computed but not stored
 """
 import os
 import shutil
@@ -51,7 +52,17 @@ def nowin(t):
     return t
 
 
-VARIANTS = {"base": lambda t: t, "nofoldmath": nofoldmath, "nofold": nofold, "noevents": noevents, "nowin": nowin}
+def nostores(t):
+    """nofold + the event records computed but not stored (the stores' own cost)"""
+    t = nofold(t)
+    t = rep(t, "    if (fs) g.qs[cur + (uint64_t)lane] = ", "    if (fs && g.gen == 0u) g.qs[cur + (uint64_t)lane] = ")
+    t = rep(t, "    if (fe) g.qe[cur + (uint64_t)lane] = ", "    if (fe && g.gen == 0u) g.qe[cur + (uint64_t)lane] = ")
+    t = rep(t, "        if (lane == 0) (t ? g.qe : g.qs)[cur + j] = r;", "        if (lane == 0 && g.gen == 0u) (t ? g.qe : g.qs)[cur + j] = r;")
+    return t
+
+
+VARIANTS = {"base": lambda t: t, "nofoldmath": nofoldmath, "nofold": nofold, "noevents": noevents, "nowin": nowin,
+            "nostores": nostores}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
